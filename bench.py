@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Headline benchmark: avg GPU utilisation + p99 scheduling latency of an FSDP
+Llama-3-8B job on MI355X (BASELINE.json metric/config).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched under torchrun, one rank per GPU over RCCL.  Rank 0 prints ONE
+JSON line.
+
+What is measured
+----------------
+1. Scheduling (rank 0, CPU only, before training): the job's GPUWorkload and a
+   stream of background workloads go through the real extender HTTP server
+   (filter -> prioritize -> bind, the kube-scheduler extender contract) over a
+   fake apiserver holding a mocked fleet of 8xMI355X nodes; pod-create -> bind
+   latencies feed a histogram whose p99 is reported (reference KPI:
+   docs/PRD.md:440; its in-process "P99" was a running max).
+2. Training: W untimed warmup steps, then exactly K timed steps bracketed by
+   barrier + synchronize; the max wall time over ranks is used.  Each rank
+   samples amd-smi gfx_activity for its GPU during the timed steps; ``value``
+   is the mean over ranks (whole-job average GPU utilisation, %).
+Synthetic tokens, random-init weights of the Llama-3-8B architecture, bf16
+compute, fp32 master weights + AdamW step inside every timed step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+BASELINE_UTIL = 87.0      # KGWE avg GPU utilisation (H100 DGX)
+BASELINE_P99_MS = 85.0    # KGWE p99 scheduling latency
+MI355X_BF16_DENSE = 2.5e15
+METRIC = ("p99 scheduling latency (ms) + avg GPU-util %, 8-GPU FSDP job on one "
+          "MI355X node")
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    ap.add_argument("--sched-pods", type=int, default=2000,
+                    help="workloads pushed through the extender for the latency p99")
+    ap.add_argument("--no-sched", action="store_true")
+    ap.add_argument("--sdpa", action="store_true", help="force PyTorch SDPA attention")
+    return ap.parse_args(argv)
+
+
+def run_scheduling_bench(args, world: int) -> dict | None:
+    try:
+        from kgwe.bench.sched_latency import run as sched_run
+    except ImportError:
+        return None
+    return sched_run(n_pods=args.sched_pods, job_gpus=world)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    import torch
+
+    from kgwe.bench.train import TrainConfig, Trainer, timed_run
+    from kgwe.ops import attn as attn_ops
+    from kgwe.parallel import dist as kdist
+
+    if args.sdpa:
+        attn_ops.set_force_sdpa(True)
+    info = kdist.init(force_group=True)
+    world = info.world_size
+    if args.gpus != world and info.is_main:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    sched = None
+    if info.is_main and not args.no_sched:
+        sched = run_scheduling_bench(args, world)
+
+    tc = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
+                     activation_checkpointing=args.ckpt)
+    tr = Trainer(tc, info)
+    res = timed_run(tr, args.steps, args.warmup)
+
+    t_max = kdist.all_reduce_max(res.seconds, info)
+    util_local = res.util_mean if res.util_mean is not None else -1.0
+    utils = [u[0] for u in kdist.all_gather_floats([util_local], info)]
+    valid = [u for u in utils if u >= 0]
+    util = sum(valid) / len(valid) if valid else None
+    tokens = tr.tokens_per_step * args.steps * world
+    tps = tokens / t_max
+    flops = tr.cfg.flops_per_token(args.seq_len) * tps
+    mfu = flops / (MI355X_BF16_DENSE * world)
+
+    if info.is_main:
+        p99 = sched["p99_ms"] if sched else None
+        out = {
+            "metric": METRIC,
+            "value": round(util, 2) if util is not None else None,
+            "unit": "% avg gfx_activity (whole job)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * t_max / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(util / BASELINE_UTIL, 4) if util is not None else None,
+            "dtype": "bf16",
+            "data": "synthetic tokens, random-init weights",
+            "config": {"model": args.model, "global_batch": args.micro_batch * world,
+                       "seq_len": args.seq_len, "parallelism": f"fsdp{world}",
+                       "micro_batch_per_gpu": args.micro_batch,
+                       "activation_checkpointing": args.ckpt},
+            "p99_sched_latency_ms": round(p99, 3) if p99 is not None else None,
+            "vs_baseline_p99": round(BASELINE_P99_MS / p99, 2) if p99 else None,
+            "sched": sched,
+            "tokens_per_s": round(tps, 1),
+            "tokens_per_s_per_gpu": round(tps / world, 1),
+            "mfu_bf16_dense": round(mfu, 4),
+            "util_per_rank": [round(u, 2) for u in utils],
+            "util_samples_rank0": res.util_samples,
+            "loss": round(res.loss, 4),
+            "peak_mem_gb_rank0": round(res.peak_mem_gb, 1),
+            "attention": "sdpa" if (args.sdpa or not attn_ops.hip_flash_available())
+            else "kgwe_flash_attn",
+        }
+        print(json.dumps(out), flush=True)
+    kdist.barrier(info)
+    kdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(main())

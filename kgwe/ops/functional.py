@@ -1,0 +1,183 @@
+"""Autograd wrappers around the gfx950 HIP kernels.
+
+Each op has a HIP path (GPU tensors, mandatory on a GPU host) and the fp32
+PyTorch reference path (CPU tensors only).  Shapes follow the Llama block in
+``kgwe.models.llama``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._lib import check, lib, ptr, stream, use_hip
+
+
+# --------------------------------------------------------------------------
+# RMSNorm (+ fused residual add)
+# --------------------------------------------------------------------------
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps, residual):
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H)
+        T = x2.shape[0]
+        y = torch.empty_like(x2)
+        rstd = torch.empty(T, device=x.device, dtype=torch.float32)
+        h = torch.empty_like(x2) if residual is not None else x2
+        r2 = residual.reshape(-1, H) if residual is not None else None
+        check(lib().kgwe_rmsnorm_fwd(ptr(x2), ptr(r2), ptr(w), ptr(y),
+                                     ptr(h) if residual is not None else None, ptr(rstd),
+                                     T, H, eps, stream(x)), "rmsnorm_fwd")
+        ctx.save_for_backward(h, w, rstd)
+        ctx.has_res = residual is not None
+        ctx.shape = x.shape
+        if residual is None:
+            return y.view(x.shape)
+        return y.view(x.shape), h.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, dh=None):
+        h, w, rstd = ctx.saved_tensors
+        H = h.shape[-1]
+        T = h.shape[0]
+        dy2 = dy.reshape(-1, H).contiguous()
+        dadd = dh.reshape(-1, H).contiguous() if dh is not None else None
+        dx = torch.empty_like(dy2)
+        G = lib().kgwe_rmsnorm_bwd_grid(T)
+        partial = torch.empty(G, H, device=h.device, dtype=torch.float32)
+        dw = torch.empty(H, device=h.device, dtype=w.dtype)
+        dw_bf = dw if w.dtype == torch.bfloat16 else None
+        dw_f = dw if w.dtype == torch.float32 else None
+        check(lib().kgwe_rmsnorm_bwd(ptr(dy2), ptr(h), ptr(w), ptr(rstd), ptr(dadd), ptr(dx),
+                                     ptr(partial), ptr(dw_bf), ptr(dw_f), T, H, stream(h)),
+              "rmsnorm_bwd")
+        dx = dx.view(ctx.shape)
+        return dx, dw, None, (dx if ctx.has_res else None)
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5,
+            residual: torch.Tensor | None = None):
+    """Returns (normed, h) where h = x + residual (the new residual stream)."""
+    if use_hip(x):
+        assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+        if residual is None:
+            return _RMSNorm.apply(x.contiguous(), w.contiguous(), eps, None), x
+        return _RMSNorm.apply(x.contiguous(), w.contiguous(), eps, residual.contiguous())
+    return ref.rmsnorm(x, w, eps, residual)
+
+
+# --------------------------------------------------------------------------
+# SwiGLU on the fused [T, 2F] gate|up projection
+# --------------------------------------------------------------------------
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        F2 = gu.shape[-1]
+        Fh = F2 // 2
+        gu2 = gu.reshape(-1, F2)
+        T = gu2.shape[0]
+        out = torch.empty(T, Fh, device=gu.device, dtype=gu.dtype)
+        check(lib().kgwe_swiglu_fwd(ptr(gu2), gu2.data_ptr() + Fh * gu2.element_size(), F2,
+                                    ptr(out), T, Fh, stream(gu)), "swiglu_fwd")
+        ctx.save_for_backward(gu2)
+        ctx.shape = gu.shape
+        return out.view(*gu.shape[:-1], Fh)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu2,) = ctx.saved_tensors
+        T, F2 = gu2.shape
+        Fh = F2 // 2
+        d2 = dout.reshape(-1, Fh).contiguous()
+        dgu = torch.empty_like(gu2)
+        es = gu2.element_size()
+        check(lib().kgwe_swiglu_bwd(ptr(gu2), gu2.data_ptr() + Fh * es, F2, ptr(d2),
+                                    ptr(dgu), dgu.data_ptr() + Fh * es, F2, T, Fh,
+                                    stream(gu2)), "swiglu_bwd")
+        return dgu.view(ctx.shape)
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    """silu(gu[..., :F]) * gu[..., F:]"""
+    if use_hip(gu):
+        return _SwiGLU.apply(gu.contiguous())
+    Fh = gu.shape[-1] // 2
+    return ref.swiglu(gu[..., :Fh], gu[..., Fh:])
+
+
+# --------------------------------------------------------------------------
+# Fused QKV split + RoPE
+# --------------------------------------------------------------------------
+class _RopeQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, seq_len, hq, hkv, d):
+        T = qkv.shape[0]
+        q = torch.empty(T, hq, d, device=qkv.device, dtype=qkv.dtype)
+        k = torch.empty(T, hkv, d, device=qkv.device, dtype=qkv.dtype)
+        v = torch.empty(T, hkv, d, device=qkv.device, dtype=qkv.dtype)
+        check(lib().kgwe_rope_qkv_fwd(ptr(qkv), ptr(q), ptr(k), ptr(v), ptr(cos), ptr(sin), T,
+                                      seq_len, hq, hkv, d, stream(qkv)), "rope_fwd")
+        ctx.save_for_backward(cos, sin)
+        ctx.meta = (T, seq_len, hq, hkv, d)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin = ctx.saved_tensors
+        T, S, hq, hkv, d = ctx.meta
+        dev = cos.device
+        dt = next(t.dtype for t in (dq, dk, dv) if t is not None)
+        z = lambda h: torch.zeros(T, h, d, device=dev, dtype=dt)  # noqa: E731
+        dq = dq.contiguous() if dq is not None else z(hq)
+        dk = dk.contiguous() if dk is not None else z(hkv)
+        dv = dv.contiguous() if dv is not None else z(hkv)
+        dqkv = torch.empty(T, (hq + 2 * hkv) * d, device=dev, dtype=dt)
+        check(lib().kgwe_rope_qkv_bwd(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(cos), ptr(sin),
+                                      T, S, hq, hkv, d, stream(dqkv)), "rope_bwd")
+        return dqkv, None, None, None, None, None, None
+
+
+def rope_qkv(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, seq_len: int,
+             hq: int, hkv: int, d: int):
+    """qkv [T, (hq+2hkv)d] -> q [T,hq,d], k [T,hkv,d], v [T,hkv,d] (rotated q, k)."""
+    if use_hip(qkv):
+        return _RopeQKV.apply(qkv.contiguous(), cos, sin, seq_len, hq, hkv, d)
+    return ref.rope_qkv(qkv, cos, sin, seq_len, hq, hkv, d)
+
+
+# --------------------------------------------------------------------------
+# Cross-entropy over the vocabulary (mean over non-ignored rows)
+# --------------------------------------------------------------------------
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        T, V = logits.shape
+        loss = torch.empty(T, device=logits.device, dtype=torch.float32)
+        lse = torch.empty(T, device=logits.device, dtype=torch.float32)
+        check(lib().kgwe_cross_entropy_fwd(ptr(logits), ptr(labels), ptr(loss), ptr(lse), T, V,
+                                           ignore_index, stream(logits)), "ce_fwd")
+        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(logits, labels, lse, n)
+        ctx.ignore_index = ignore_index
+        return loss.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, lse, n = ctx.saved_tensors
+        T, V = logits.shape
+        scale = (g.to(torch.float32) / n).reshape(1).contiguous()
+        dlogits = torch.empty_like(logits)
+        check(lib().kgwe_cross_entropy_bwd(ptr(logits), ptr(labels), ptr(lse), ptr(scale),
+                                           ptr(dlogits), T, V, ctx.ignore_index,
+                                           stream(logits)), "ce_bwd")
+        return dlogits, None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100):
+    logits = logits.reshape(-1, logits.shape[-1])
+    labels = labels.reshape(-1)
+    if use_hip(logits):
+        assert logits.shape[-1] % 8 == 0, "vocab must be a multiple of 8 (16-B rows)"
+        return _CrossEntropy.apply(logits.contiguous(), labels.to(torch.int64).contiguous(),
+                                   ignore_index)
+    return ref.cross_entropy(logits, labels, ignore_index)
