@@ -7,6 +7,8 @@ sampling) and by ``__graft_entry__.smoke``.
 """
 from __future__ import annotations
 
+import os
+import sys
 import time
 from dataclasses import dataclass
 
@@ -30,6 +32,14 @@ class TrainConfig:
     seed: int = 1234
 
 
+_T0 = time.perf_counter()
+
+
+def log(info, msg: str) -> None:
+    if info.rank == 0 and os.environ.get("KGWE_QUIET") != "1":
+        print(f"[kgwe {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 class Trainer:
     def __init__(self, tc: TrainConfig, info: kdist.DistInfo):
         self.tc = tc
@@ -37,12 +47,14 @@ class Trainer:
         self.cfg = llama.PRESETS[tc.model]
         dev = info.device
         torch.manual_seed(tc.seed)
+        log(info, f"building {tc.model} ({self.cfg.num_params() / 1e9:.2f}B params) on {dev}")
         self.model = llama.build(self.cfg, device=dev, dtype=torch.float32)
         self.model.activation_checkpointing = tc.activation_checkpointing
         if tc.fsdp:
             if not torch.distributed.is_initialized():
                 raise RuntimeError("FSDP needs a process group: kdist.init(force_group=True)")
             shard_model(self.model)
+            log(info, f"FSDP2 sharded over {info.world_size} rank(s)")
         self.opt = FusedAdamW(self.model.parameters(), lr=tc.lr)
         g = torch.Generator(device=dev).manual_seed(tc.seed + info.rank)
         self.tokens = torch.randint(0, self.cfg.vocab_size, (tc.micro_batch, tc.seq_len + 1),
@@ -81,9 +93,11 @@ class RunResult:
 
 def timed_run(tr: Trainer, steps: int, warmup: int, sample_util: bool = True) -> RunResult:
     info = tr.info
-    for _ in range(warmup):
+    for i in range(warmup):
+        t = time.perf_counter()
         tr.step()
-    tr.sync()
+        tr.sync()
+        log(info, f"warmup step {i}: {time.perf_counter() - t:.3f}s")
     kdist.barrier(info)
     tr.sync()
     sampler = UtilSampler(info.local_rank if info.device.type == "cuda" else 0)
@@ -93,6 +107,7 @@ def timed_run(tr: Trainer, steps: int, warmup: int, sample_util: bool = True) ->
     for _ in range(steps):
         tr.step()
     tr.sync()
+    log(info, f"timed {steps} steps: {time.perf_counter() - t0:.3f}s")
     kdist.barrier(info)
     tr.sync()
     dt = time.perf_counter() - t0

@@ -1,0 +1,154 @@
+// kgwe data model (L1): MI355X devices, xGMI links, compute/memory partitions,
+// node and cluster topology snapshots.
+//
+// Parity map to the reference's Go types (src/discovery/types.go):
+//   GPUDevice (:11-47)        -> GpuDevice
+//   GPUMemory (:62-80)        -> memory_total_mb / memory_used_mb / hbm_bw_gbps
+//   DeviceTopology (:116-131) -> numa_node, cpu_affinity, pcie, links
+//   NVLinkInfo (:134-146)     -> XgmiLink (per peer, measured + rated GB/s)
+//   MIGConfiguration (:167-230) -> PartitionConfig (SPX/DPX/QPX/CPX x NPS)
+//   GPUUtilization (:242-266) -> Utilization (gfx_activity, umc_activity, ...)
+//   GPUHealth (:269-321)      -> Health (RAS/ECC, xGMI errors, throttle)
+//   NodeTopology (:351-366)   -> NodeTopology
+//   ClusterTopology (:336-348)-> ClusterTopology (immutable snapshot)
+// Everything is MI355X vocabulary: no NVLink / NVSwitch / MIG / NVML fields.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "json.h"
+
+namespace kgwe {
+
+enum class HealthStatus { Healthy, Degraded, Unhealthy, Unknown };
+enum class LinkType { XGMI, PCIE, Unknown };
+enum class ComputePartition { SPX, DPX, TPX, QPX, CPX };
+enum class MemoryPartition { NPS1, NPS2, NPS4, NPS8 };
+
+const char* to_string(HealthStatus s);
+const char* to_string(LinkType t);
+const char* to_string(ComputePartition p);
+const char* to_string(MemoryPartition p);
+HealthStatus health_from(const std::string& s);
+LinkType link_from(const std::string& s);
+ComputePartition compute_partition_from(const std::string& s);
+MemoryPartition memory_partition_from(const std::string& s);
+int partition_count(ComputePartition p);  // SPX 1, DPX 2, TPX 3, QPX 4, CPX 8
+
+struct XgmiLink {
+  std::string peer_uuid;
+  LinkType type = LinkType::XGMI;
+  int hops = 1;
+  double rated_gbps = 153.6;   // per-direction rated xGMI link bandwidth
+  double measured_gbps = 0.0;  // from the HIP pull probe (0 = not measured)
+  bool up = true;
+  // Effective bandwidth used by scorers: measured when available, else rated.
+  double effective_gbps() const { return measured_gbps > 0 ? measured_gbps : rated_gbps; }
+};
+
+struct PcieInfo {
+  std::string bdf;
+  std::string switch_id;
+  int generation = 5;
+  int width = 16;
+  double bandwidth_gbps = 63.0;  // Gen5 x16
+};
+
+struct Utilization {
+  double gfx_activity = 0.0;  // % — THE "GPU utilisation" on MI355X
+  double umc_activity = 0.0;  // % memory controller busy
+  double memory_used_pct = 0.0;
+  double power_w = 0.0;
+  double temperature_c = 0.0;
+  double gfx_clock_mhz = 0.0;
+};
+
+struct Health {
+  HealthStatus status = HealthStatus::Healthy;
+  std::vector<std::string> reasons;
+  int64_t ecc_correctable = 0;
+  int64_t ecc_uncorrectable = 0;
+  int64_t ecc_deferred = 0;
+  int xgmi_errors = 0;
+  std::vector<std::string> throttle_reasons;
+};
+
+// One schedulable slice of a partitioned GPU (CPX: 8 per GPU, one per XCD).
+struct PartitionInstance {
+  std::string id;  // "<gpu uuid>/p<index>"
+  int index = 0;
+  int cu_count = 256;
+  double memory_gb = 288.0;
+  bool in_use = false;
+  std::string owner;  // workload uid
+};
+
+struct PartitionConfig {
+  ComputePartition compute = ComputePartition::SPX;
+  MemoryPartition memory = MemoryPartition::NPS1;
+  bool switching = false;  // reconfiguration in flight (drain -> switch)
+  std::vector<PartitionInstance> instances;
+};
+
+struct GpuDevice {
+  std::string uuid;
+  int index = 0;
+  std::string node;
+  std::string model = "AMD Instinct MI355X";
+  std::string arch = "gfx950";
+  int cu_count = 256;
+  int xcd_count = 8;
+  double memory_total_gb = 288.0;
+  double memory_used_gb = 0.0;
+  double hbm_rated_gbps = 8000.0;
+  double hbm_measured_gbps = 0.0;
+  double peak_bf16_tflops = 2500.0;
+  int numa_node = 0;
+  int socket = 0;
+  PcieInfo pcie;
+  std::vector<XgmiLink> links;
+  PartitionConfig partition;
+  Utilization util;
+  Health health;
+
+  double memory_free_gb() const { return memory_total_gb - memory_used_gb; }
+  const XgmiLink* link_to(const std::string& peer) const;
+  bool healthy() const { return health.status == HealthStatus::Healthy; }
+};
+
+struct NodeTopology {
+  std::string name;
+  std::map<std::string, std::string> labels;
+  std::vector<std::pair<std::string, std::string>> taints;  // key=value:effect
+  std::vector<GpuDevice> gpus;
+  int numa_nodes = 2;
+  int cpu_sockets = 2;
+  bool xgmi_fully_connected = true;
+  int64_t updated_ns = 0;
+
+  const GpuDevice* gpu(const std::string& uuid) const;
+  GpuDevice* gpu(const std::string& uuid);
+};
+
+struct ClusterTopology {
+  std::map<std::string, NodeTopology> nodes;
+  uint64_t generation = 0;
+  int64_t updated_ns = 0;
+  int total_gpus() const;
+};
+
+using TopologySnapshot = std::shared_ptr<const ClusterTopology>;
+
+// JSON <-> model (fixture format == snapshot export format).
+GpuDevice gpu_from_json(const Json& j, const std::string& node);
+Json to_json(const GpuDevice& g);
+NodeTopology node_from_json(const Json& j);
+Json to_json(const NodeTopology& n);
+Json to_json(const ClusterTopology& c);
+
+int64_t now_ns();
+
+}  // namespace kgwe

@@ -1,0 +1,1319 @@
+#include "scheduler.h"
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+#include <numeric>
+
+namespace kgwe {
+
+// ---------------------------------------------------------------------------
+// enums
+// ---------------------------------------------------------------------------
+const char* to_string(TopologyPreference p) {
+  switch (p) {
+    case TopologyPreference::None: return "None";
+    case TopologyPreference::XgmiOptimal: return "xGMIOptimal";
+    case TopologyPreference::XgmiRequired: return "xGMIRequired";
+    case TopologyPreference::SameNUMA: return "SameNUMA";
+    case TopologyPreference::SamePCIeSwitch: return "SamePCIeSwitch";
+  }
+  return "None";
+}
+TopologyPreference topology_preference_from(const std::string& s) {
+  if (s == "xGMIOptimal" || s == "XGMIOptimal" || s == "NVLinkOptimal")
+    return TopologyPreference::XgmiOptimal;
+  if (s == "xGMIRequired" || s == "XGMIRequired" || s == "NVLinkRequired")
+    return TopologyPreference::XgmiRequired;
+  if (s == "SameNUMA") return TopologyPreference::SameNUMA;
+  if (s == "SamePCIeSwitch") return TopologyPreference::SamePCIeSwitch;
+  return TopologyPreference::None;
+}
+const char* to_string(WorkloadType t) {
+  switch (t) {
+    case WorkloadType::Training: return "Training";
+    case WorkloadType::Inference: return "Inference";
+    case WorkloadType::Batch: return "Batch";
+    case WorkloadType::Interactive: return "Interactive";
+    case WorkloadType::Development: return "Development";
+    default: return "Unknown";
+  }
+}
+WorkloadType workload_type_from(const std::string& s) {
+  if (s == "Training") return WorkloadType::Training;
+  if (s == "Inference") return WorkloadType::Inference;
+  if (s == "Batch") return WorkloadType::Batch;
+  if (s == "Interactive") return WorkloadType::Interactive;
+  if (s == "Development") return WorkloadType::Development;
+  return s.empty() ? WorkloadType::Training : WorkloadType::Unknown;
+}
+const char* to_string(DistributionStrategy s) {
+  switch (s) {
+    case DistributionStrategy::None: return "None";
+    case DistributionStrategy::DataParallel: return "DataParallel";
+    case DistributionStrategy::ModelParallel: return "ModelParallel";
+    case DistributionStrategy::PipelineParallel: return "PipelineParallel";
+    case DistributionStrategy::Hybrid: return "Hybrid";
+    case DistributionStrategy::FSDP: return "FSDP";
+    case DistributionStrategy::DeepSpeed: return "DeepSpeed";
+    case DistributionStrategy::ContextParallel: return "ContextParallel";
+    case DistributionStrategy::ExpertParallel: return "ExpertParallel";
+  }
+  return "None";
+}
+DistributionStrategy strategy_from(const std::string& s) {
+  if (s == "DataParallel" || s == "DDP") return DistributionStrategy::DataParallel;
+  if (s == "ModelParallel" || s == "TensorParallel") return DistributionStrategy::ModelParallel;
+  if (s == "PipelineParallel") return DistributionStrategy::PipelineParallel;
+  if (s == "Hybrid") return DistributionStrategy::Hybrid;
+  if (s == "FSDP") return DistributionStrategy::FSDP;
+  if (s == "DeepSpeed") return DistributionStrategy::DeepSpeed;
+  if (s == "ContextParallel" || s == "SequenceParallel") return DistributionStrategy::ContextParallel;
+  if (s == "ExpertParallel") return DistributionStrategy::ExpertParallel;
+  return DistributionStrategy::None;
+}
+const char* to_string(CommBackend b) {
+  switch (b) {
+    case CommBackend::RCCL: return "RCCL";
+    case CommBackend::Gloo: return "Gloo";
+    case CommBackend::MPI: return "MPI";
+  }
+  return "RCCL";
+}
+CommBackend backend_from(const std::string& s) {
+  if (s == "Gloo" || s == "gloo") return CommBackend::Gloo;
+  if (s == "MPI" || s == "mpi") return CommBackend::MPI;
+  return CommBackend::RCCL;  // "RCCL", "NCCL" (alias: RCCL implements the NCCL API)
+}
+const char* to_string(SchedEventType t) {
+  switch (t) {
+    case SchedEventType::Scheduled: return "Scheduled";
+    case SchedEventType::Failed: return "Failed";
+    case SchedEventType::Released: return "Released";
+    case SchedEventType::Preempted: return "Preempted";
+    case SchedEventType::GangReady: return "GangReady";
+    case SchedEventType::GangTimeout: return "GangTimeout";
+  }
+  return "Unknown";
+}
+
+// ---------------------------------------------------------------------------
+// JSON <-> WorkloadRequest (GPUWorkload custom resource or bare spec)
+// ---------------------------------------------------------------------------
+static std::vector<std::string> str_list(const Json& j) {
+  std::vector<std::string> v;
+  for (const auto& e : j.items()) v.push_back(e.str());
+  return v;
+}
+
+static std::vector<AffinityTerm> terms_from(const Json& j) {
+  std::vector<AffinityTerm> out;
+  for (const auto& t : j.items()) {
+    AffinityTerm a;
+    a.key = t.get("key").str();
+    a.op = t.get("operator").str("In");
+    a.values = str_list(t.get("values"));
+    a.weight = static_cast<int>(t.get("weight").as_int(0));
+    out.push_back(a);
+  }
+  return out;
+}
+
+WorkloadRequest workload_from_json(const Json& in) {
+  WorkloadRequest w;
+  const Json& meta = in.get("metadata");
+  const Json& spec = in.has("spec") ? in.get("spec") : in;
+  w.uid = meta.get("uid").str(in.get("uid").str());
+  w.name = meta.get("name").str(in.get("name").str());
+  w.ns = meta.get("namespace").str(in.get("namespace").str("default"));
+  if (w.uid.empty()) w.uid = w.ns + "/" + w.name;
+  const Json& labels = meta.get("labels");
+  w.team = spec.get("team").str(labels.get("kgwe.amd.com/team").str(labels.get("team").str()));
+  w.project = spec.get("project").str(labels.get("kgwe.amd.com/project").str());
+  const Json& req = spec.has("gpuRequirements") ? spec.get("gpuRequirements") : spec;
+  w.gpu_count = static_cast<int>(req.get("count").as_int(req.get("gpuCount").as_int(1)));
+  w.min_memory_gb = req.get("minMemoryGB").as_number(0.0);
+  w.min_bandwidth_gbps = req.get("minBandwidthGBps").as_number(0.0);
+  const Json& topo = req.get("topology");
+  if (topo.is_object()) {
+    w.topology = topology_preference_from(topo.get("preference").str("None"));
+    if (topo.has("minBandwidthGBps"))
+      w.min_bandwidth_gbps = std::max(w.min_bandwidth_gbps, topo.get("minBandwidthGBps").as_number());
+  } else if (topo.is_string()) {
+    w.topology = topology_preference_from(topo.str());
+  }
+  w.arch = req.get("architecture").str();
+  w.model = req.get("gpuModel").str();
+  const Json& part = req.get("partition");
+  if (part.is_object()) {
+    w.partition = true;
+    w.partition_mode = compute_partition_from(part.get("mode").str("CPX"));
+    w.partition_count = static_cast<int>(part.get("count").as_int(1));
+  }
+  const Json& mig = req.get("mig");  // legacy MIG field: map profile size to a mode
+  if (!w.partition && mig.is_object()) {
+    const std::string prof = mig.get("profile").str();
+    w.partition = true;
+    w.partition_count = static_cast<int>(mig.get("count").as_int(1));
+    if (prof.rfind("1g", 0) == 0) w.partition_mode = ComputePartition::CPX;
+    else if (prof.rfind("2g", 0) == 0) w.partition_mode = ComputePartition::QPX;
+    else if (prof.rfind("3g", 0) == 0 || prof.rfind("4g", 0) == 0) w.partition_mode = ComputePartition::DPX;
+    else w.partition_mode = ComputePartition::SPX;
+  }
+  w.type = workload_type_from(spec.get("workloadType").str("Training"));
+  w.framework = spec.get("framework").str("PyTorch");
+  const Json& dc = spec.get("distributedConfig");
+  w.strategy = strategy_from(dc.get("strategy").str("None"));
+  w.world_size = static_cast<int>(dc.get("worldSize").as_int(0));
+  w.backend = backend_from(dc.get("backend").str("RCCL"));
+  w.priority = spec.get("priority").as_int(0);
+  w.preemptible = spec.get("preemptible").as_bool(true);
+  const Json& c = spec.has("constraints") ? spec.get("constraints") : spec;
+  for (const auto& kv : c.get("nodeSelector").fields()) w.node_selector[kv.first] = kv.second.str();
+  const Json& aff = c.get("affinity");
+  w.required_affinity = terms_from(aff.get("required"));
+  w.preferred_affinity = terms_from(aff.get("preferred"));
+  for (const auto& t : c.get("tolerations").items()) {
+    Toleration tl;
+    tl.key = t.get("key").str();
+    tl.op = t.get("operator").str("Equal");
+    tl.value = t.get("value").str();
+    tl.effect = t.get("effect").str();
+    w.tolerations.push_back(tl);
+  }
+  w.exclude_nodes = str_list(c.get("excludeNodes"));
+  w.colocate_with = str_list(c.get("colocateWith"));
+  w.anti_affinity_with = str_list(c.get("antiAffinityWith"));
+  w.max_latency_ms = c.get("maxLatencyMs").as_number(0.0);
+  const Json& gang = spec.get("gang");
+  if (gang.is_object()) {
+    w.gang = gang.get("name").str();
+    w.gang_size = static_cast<int>(gang.get("size").as_int(0));
+  }
+  w.preferred_nodes = str_list(spec.get("preferredNodes"));
+  return w;
+}
+
+Json to_json(const WorkloadRequest& w) {
+  Json j = Json::object();
+  j["uid"] = w.uid;
+  j["name"] = w.name;
+  j["namespace"] = w.ns;
+  j["team"] = w.team;
+  j["gpu_count"] = w.gpu_count;
+  j["min_memory_gb"] = w.min_memory_gb;
+  j["min_bandwidth_gbps"] = w.min_bandwidth_gbps;
+  j["topology"] = to_string(w.topology);
+  j["partition"] = w.partition;
+  if (w.partition) {
+    j["partition_mode"] = to_string(w.partition_mode);
+    j["partition_count"] = w.partition_count;
+  }
+  j["type"] = to_string(w.type);
+  j["strategy"] = to_string(w.strategy);
+  j["backend"] = to_string(w.backend);
+  j["world_size"] = w.world_size;
+  j["priority"] = w.priority;
+  j["preemptible"] = w.preemptible;
+  j["gang"] = w.gang;
+  j["gang_size"] = w.gang_size;
+  return j;
+}
+
+Json to_json(const Decision& d) {
+  Json j = Json::object();
+  j["ok"] = d.ok;
+  j["status"] = d.status;
+  j["uid"] = d.uid;
+  j["node"] = d.node;
+  Json g = Json::array();
+  for (const auto& x : d.gpus) g.push_back(x);
+  j["gpus"] = g;
+  Json p = Json::array();
+  for (const auto& x : d.partitions) p.push_back(x);
+  j["partitions"] = p;
+  j["score"] = d.score;
+  j["bandwidth_gbps"] = d.bandwidth_gbps;
+  j["latency_ms"] = d.latency_ms;
+  Json r = Json::array();
+  for (const auto& x : d.reasons) r.push_back(x);
+  j["reasons"] = r;
+  Json pr = Json::array();
+  for (const auto& x : d.preempted) pr.push_back(x);
+  j["preempted"] = pr;
+  Json f = Json::object();
+  for (const auto& kv : d.failed_nodes) f[kv.first] = kv.second;
+  j["failed_nodes"] = f;
+  return j;
+}
+
+Json to_json(const Allocation& a) {
+  Json j = Json::object();
+  j["uid"] = a.uid;
+  j["node"] = a.node;
+  j["namespace"] = a.ns;
+  j["team"] = a.team;
+  j["gang"] = a.gang;
+  Json g = Json::array();
+  for (const auto& x : a.gpus) g.push_back(x);
+  j["gpus"] = g;
+  Json p = Json::array();
+  for (const auto& x : a.partitions) p.push_back(x);
+  j["partitions"] = p;
+  j["type"] = to_string(a.type);
+  j["priority"] = a.priority;
+  j["preemptible"] = a.preemptible;
+  j["gang_pending"] = a.gang_pending;
+  j["bandwidth_gbps"] = a.bandwidth_gbps;
+  return j;
+}
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+namespace {
+
+bool term_matches(const AffinityTerm& t, const std::map<std::string, std::string>& labels) {
+  auto it = labels.find(t.key);
+  const bool has = it != labels.end();
+  if (t.op == "Exists") return has;
+  if (t.op == "DoesNotExist") return !has;
+  if (t.op == "In") return has && std::find(t.values.begin(), t.values.end(), it->second) != t.values.end();
+  if (t.op == "NotIn") return !has || std::find(t.values.begin(), t.values.end(), it->second) == t.values.end();
+  if ((t.op == "Gt" || t.op == "Lt") && has && !t.values.empty()) {
+    try {
+      const double a = std::stod(it->second), b = std::stod(t.values[0]);
+      return t.op == "Gt" ? a > b : a < b;
+    } catch (...) {
+      return false;
+    }
+  }
+  return false;
+}
+
+bool tolerated(const std::string& kv, const std::string& effect, const std::vector<Toleration>& ts) {
+  auto eq = kv.find('=');
+  const std::string key = kv.substr(0, eq);
+  const std::string val = eq == std::string::npos ? "" : kv.substr(eq + 1);
+  for (const auto& t : ts) {
+    if (!t.effect.empty() && t.effect != effect) continue;
+    if (t.op == "Exists" && (t.key.empty() || t.key == key)) return true;
+    if (t.key == key && t.value == val) return true;
+  }
+  return false;
+}
+
+double pair_bw(const GpuDevice& a, const GpuDevice& b, bool* xgmi_up) {
+  const XgmiLink* l1 = a.link_to(b.uuid);
+  const XgmiLink* l2 = b.link_to(a.uuid);
+  const bool up1 = l1 && l1->up && l1->type == LinkType::XGMI;
+  const bool up2 = l2 ? (l2->up && l2->type == LinkType::XGMI) : up1;
+  if (up1 && up2) {
+    *xgmi_up = true;
+    double bw = l1->effective_gbps();
+    if (l2) bw = std::min(bw, l2->effective_gbps());
+    return bw;
+  }
+  *xgmi_up = false;
+  return std::min(a.pcie.bandwidth_gbps, b.pcie.bandwidth_gbps);
+}
+
+// Visit every k-combination of [0, n) (lexicographic), stop when f returns false.
+void for_each_combination(int n, int k, const std::function<bool(const std::vector<int>&)>& f) {
+  if (k > n || k <= 0) return;
+  std::vector<int> idx(k);
+  std::iota(idx.begin(), idx.end(), 0);
+  for (;;) {
+    if (!f(idx)) return;
+    int i = k - 1;
+    while (i >= 0 && idx[i] == n - k + i) --i;
+    if (i < 0) return;
+    ++idx[i];
+    for (int j = i + 1; j < k; ++j) idx[j] = idx[j - 1] + 1;
+  }
+}
+
+double n_choose_k(int n, int k) {
+  if (k < 0 || k > n) return 0;
+  double r = 1;
+  for (int i = 1; i <= k; ++i) r = r * (n - k + i) / i;
+  return r;
+}
+
+bool comm_heavy(DistributionStrategy s) {
+  return s == DistributionStrategy::ModelParallel || s == DistributionStrategy::ContextParallel ||
+         s == DistributionStrategy::ExpertParallel;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Scheduler
+// ---------------------------------------------------------------------------
+Scheduler::Scheduler(std::shared_ptr<DiscoveryService> disc, SchedulerConfig cfg)
+    : disc_(std::move(disc)), cfg_(cfg) {}
+
+void Scheduler::set_config(const SchedulerConfig& c) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  cfg_ = c;
+}
+
+// Caller holds mu_ (shared or unique).
+std::vector<const GpuDevice*> Scheduler::free_gpus(const NodeTopology& n,
+                                                   const WorkloadRequest& w) const {
+  std::vector<const GpuDevice*> out;
+  for (const auto& g : n.gpus) {
+    if (!g.healthy()) continue;
+    if (g.partition.compute != ComputePartition::SPX || g.partition.switching) continue;
+    if (gpu_owner_.count(g.uuid)) continue;
+    if (g.memory_free_gb() + 1e-9 < w.min_memory_gb) continue;
+    if (!w.arch.empty() && g.arch != w.arch) continue;
+    if (!w.model.empty() && g.model.find(w.model) == std::string::npos) continue;
+    out.push_back(&g);
+  }
+  return out;
+}
+
+std::vector<const PartitionInstance*> Scheduler::free_partitions(
+    const NodeTopology& n, const WorkloadRequest& w, std::vector<std::string>* gpu_of) const {
+  std::vector<const PartitionInstance*> out;
+  for (const auto& g : n.gpus) {
+    if (!g.healthy() || g.partition.switching) continue;
+    if (g.partition.compute != w.partition_mode) continue;
+    if (!w.arch.empty() && g.arch != w.arch) continue;
+    if (gpu_owner_.count(g.uuid)) continue;  // whole GPU taken
+    for (const auto& pi : g.partition.instances) {
+      if (pi.in_use || part_owner_.count(pi.id)) continue;
+      if (pi.memory_gb + 1e-9 < w.min_memory_gb) continue;
+      out.push_back(&pi);
+      if (gpu_of) gpu_of->push_back(g.uuid);
+    }
+  }
+  return out;
+}
+
+std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w) const {
+  if (std::find(w.exclude_nodes.begin(), w.exclude_nodes.end(), n.name) != w.exclude_nodes.end())
+    return "node excluded by workload";
+  for (const auto& kv : w.node_selector) {
+    auto it = n.labels.find(kv.first);
+    if (it == n.labels.end() || it->second != kv.second)
+      return "node selector mismatch: " + kv.first + "=" + kv.second;
+  }
+  for (const auto& t : w.required_affinity)
+    if (!term_matches(t, n.labels)) return "required node affinity not satisfied: " + t.key;
+  for (const auto& t : n.taints) {
+    if (t.second != "NoSchedule" && t.second != "NoExecute") continue;
+    if (!tolerated(t.first, t.second, w.tolerations))
+      return "untolerated taint " + t.first + ":" + t.second;
+  }
+  for (const auto& other : w.anti_affinity_with) {
+    auto it = allocs_.find(other);
+    if (it != allocs_.end() && it->second.node == n.name) return "anti-affinity with " + other;
+  }
+  for (const auto& other : w.colocate_with) {
+    auto it = allocs_.find(other);
+    if (it != allocs_.end() && it->second.node != n.name)
+      return "must co-locate with " + other + " on " + it->second.node;
+  }
+  if (w.partition) {
+    auto parts = free_partitions(n, w, nullptr);
+    if (static_cast<int>(parts.size()) < w.partition_count)
+      return "insufficient free " + std::string(to_string(w.partition_mode)) + " partitions (" +
+             std::to_string(parts.size()) + " < " + std::to_string(w.partition_count) + ")";
+    return "";
+  }
+  auto avail = free_gpus(n, w);
+  if (static_cast<int>(avail.size()) < w.gpu_count)
+    return "insufficient free GPUs (" + std::to_string(avail.size()) + " < " +
+           std::to_string(w.gpu_count) + ")";
+  const bool need_clique = w.topology == TopologyPreference::XgmiRequired ||
+                           (comm_heavy(w.strategy) && w.topology == TopologyPreference::None);
+  if (w.gpu_count > 1 && (need_clique || w.min_bandwidth_gbps > 0)) {
+    std::vector<std::string> sel;
+    double bw = 0.0;
+    bool clique = false;
+    topology_score(n, avail, w, &sel, &bw, &clique);
+    if (need_clique && !clique) return "no fully connected xGMI group of " + std::to_string(w.gpu_count);
+    if (w.min_bandwidth_gbps > 0) {
+      // min pairwise bandwidth of the chosen group
+      double mn = 1e30;
+      for (size_t i = 0; i < sel.size(); ++i)
+        for (size_t j = i + 1; j < sel.size(); ++j) {
+          bool up = false;
+          mn = std::min(mn, pair_bw(*n.gpu(sel[i]), *n.gpu(sel[j]), &up));
+        }
+      if (mn < w.min_bandwidth_gbps)
+        return "group bandwidth " + std::to_string(static_cast<int>(mn)) + " GB/s < required " +
+               std::to_string(static_cast<int>(w.min_bandwidth_gbps));
+    }
+  }
+  return "";
+}
+
+// xGMI-aware group selection + topology score (see header).
+int Scheduler::topology_score(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
+                              const WorkloadRequest& w, std::vector<std::string>* sel, double* bw_out,
+                              bool* clique_out) const {
+  const int k = w.gpu_count;
+  sel->clear();
+  *bw_out = 0.0;
+  *clique_out = false;
+  if (static_cast<int>(avail.size()) < k || k <= 0) return 0;
+  // Free GPUs per NUMA domain / PCIe switch (fragmentation + locality terms).
+  std::map<int, int> free_numa, total_numa;
+  for (const auto& g : n.gpus) total_numa[g.numa_node]++;
+  for (auto* g : avail) free_numa[g->numa_node]++;
+
+  if (k == 1) {
+    // Best fit: the GPU in the NUMA domain with the FEWEST free GPUs (keeps
+    // whole domains / large cliques free), then the one with the most
+    // degraded links (least useful for future multi-GPU jobs).
+    const GpuDevice* best = nullptr;
+    std::tuple<int, int, int> bkey{1 << 30, 0, 0};
+    for (auto* g : avail) {
+      int degraded = 0;
+      for (const auto& l : g->links)
+        if (!l.up || (l.measured_gbps > 0 && l.measured_gbps < cfg_.degraded_link_ratio * l.rated_gbps))
+          ++degraded;
+      std::tuple<int, int, int> key{free_numa[g->numa_node], -degraded, g->index};
+      if (!best || key < bkey) {
+        best = g;
+        bkey = key;
+      }
+    }
+    sel->push_back(best->uuid);
+    *clique_out = true;
+    return 100;
+  }
+
+  const int m = static_cast<int>(avail.size());
+  // Minimal number of NUMA domains a k-group can span.
+  std::vector<int> sizes;
+  for (auto& kv : free_numa) sizes.push_back(kv.second);
+  std::sort(sizes.rbegin(), sizes.rend());
+  int need_domains = 0;
+  for (int acc = 0; acc < k && need_domains < static_cast<int>(sizes.size()); ++need_domains)
+    acc += sizes[need_domains];
+
+  struct Best {
+    double obj = -1e30;
+    std::vector<int> idx;
+    double agg = 0, minbw = 0;
+    bool clique = false;
+    int domains = 0;
+  } best;
+  const double ideal = cfg_.rated_link_gbps * k * (k - 1) / 2.0;
+  const std::string pref_switch;
+  auto evaluate = [&](const std::vector<int>& idx) {
+    double agg = 0.0, minbw = 1e30;
+    bool clique = true;
+    std::map<int, int> used_numa;
+    std::set<std::string> switches;
+    for (size_t i = 0; i < idx.size(); ++i) {
+      const GpuDevice* a = avail[idx[i]];
+      used_numa[a->numa_node]++;
+      switches.insert(a->pcie.switch_id);
+      for (size_t j = i + 1; j < idx.size(); ++j) {
+        bool up = false;
+        double bw = pair_bw(*a, *avail[idx[j]], &up);
+        clique &= up;
+        agg += bw;
+        minbw = std::min(minbw, bw);
+      }
+    }
+    // Fragmentation: whole NUMA domains left completely free after placement.
+    int whole_free_after = 0;
+    for (auto& kv : total_numa) {
+      int left = free_numa[kv.first] - used_numa[kv.first];
+      if (left == kv.second) ++whole_free_after;
+    }
+    const int domains = static_cast<int>(used_numa.size());
+    double obj = (clique ? 1000.0 : 0.0) + 300.0 * std::min(1.0, agg / ideal) +
+                 100.0 * (need_domains > 0 ? static_cast<double>(need_domains) / domains : 1.0) +
+                 20.0 * whole_free_after + 5.0 * (minbw / cfg_.rated_link_gbps);
+    if (w.topology == TopologyPreference::SamePCIeSwitch) obj += switches.size() == 1 ? 500.0 : 0.0;
+    if (w.topology == TopologyPreference::SameNUMA) obj += domains == 1 ? 500.0 : 0.0;
+    if (obj > best.obj) {
+      best.obj = obj;
+      best.idx = idx;
+      best.agg = agg;
+      best.minbw = minbw;
+      best.clique = clique;
+      best.domains = domains;
+    }
+    return true;
+  };
+  if (n_choose_k(m, k) <= static_cast<double>(cfg_.exhaustive_limit)) {
+    for_each_combination(m, k, evaluate);
+  } else {
+    // Greedy clique growth from every start GPU (reference-style search,
+    // but on effective bandwidth and with the same objective to pick).
+    for (int s = 0; s < m; ++s) {
+      std::vector<int> grp{s};
+      std::vector<bool> in(m, false);
+      in[s] = true;
+      while (static_cast<int>(grp.size()) < k) {
+        int pick = -1;
+        double pick_bw = -1;
+        for (int c = 0; c < m; ++c) {
+          if (in[c]) continue;
+          double aggc = 0;
+          bool ok = true;
+          for (int g : grp) {
+            bool up = false;
+            aggc += pair_bw(*avail[c], *avail[g], &up);
+            ok &= up;
+          }
+          double keyv = (ok ? 1e6 : 0) + aggc + (avail[c]->numa_node == avail[s]->numa_node ? 1 : 0);
+          if (keyv > pick_bw) {
+            pick = c;
+            pick_bw = keyv;
+          }
+        }
+        grp.push_back(pick);
+        in[pick] = true;
+      }
+      std::sort(grp.begin(), grp.end());
+      evaluate(grp);
+    }
+  }
+  for (int i : best.idx) sel->push_back(avail[i]->uuid);
+  const int pairs = k * (k - 1) / 2;
+  *bw_out = pairs ? best.agg / pairs : 0.0;
+  *clique_out = best.clique;
+  const double bwn = std::min(1.0, best.agg / ideal);
+  const double numa_term = need_domains > 0 ? static_cast<double>(need_domains) / best.domains : 1.0;
+  switch (w.topology) {
+    case TopologyPreference::None:
+      return 50;
+    case TopologyPreference::SameNUMA:
+      return best.domains == 1 ? 90 : 50;
+    case TopologyPreference::SamePCIeSwitch: {
+      std::set<std::string> sw;
+      for (int i : best.idx) sw.insert(avail[i]->pcie.switch_id);
+      return sw.size() == 1 ? 80 : 40;
+    }
+    default:
+      break;
+  }
+  if (!best.clique) return static_cast<int>(30.0 * bwn);
+  return static_cast<int>(std::lround(60.0 + 25.0 * bwn + 15.0 * numa_term));
+}
+
+// The reference's scorer, kept verbatim in behaviour for A/B (ScoringMode::Compat):
+// NVLink-style greedy clique normalised to 900 GB/s per pair, NUMA 90/50,
+// PCIe switch 80/40, None 50 with the first k GPUs.
+int Scheduler::topology_score_compat(const NodeTopology& n,
+                                     const std::vector<const GpuDevice*>& avail,
+                                     const WorkloadRequest& w, std::vector<std::string>* sel) const {
+  const int k = w.gpu_count;
+  sel->clear();
+  if (k <= 1) {
+    if (avail.empty()) return 0;
+    sel->push_back(avail[0]->uuid);
+    return 100;
+  }
+  if (static_cast<int>(avail.size()) < k) return 0;
+  auto first_k = [&]() {
+    for (int i = 0; i < k; ++i) sel->push_back(avail[i]->uuid);
+  };
+  switch (w.topology) {
+    case TopologyPreference::XgmiOptimal:
+    case TopologyPreference::XgmiRequired: {
+      std::vector<std::string> best;
+      double best_bw = 0.0;
+      for (auto* start : avail) {
+        std::vector<const GpuDevice*> grp{start};
+        double tot = 0.0;
+        while (static_cast<int>(grp.size()) < k) {
+          const GpuDevice* cand = nullptr;
+          double cand_bw = 0.0;
+          for (auto* c : avail) {
+            if (std::find(grp.begin(), grp.end(), c) != grp.end()) continue;
+            double agg = 0.0;
+            bool full = true;
+            for (auto* m : grp) {
+              const XgmiLink* l = c->link_to(m->uuid);
+              if (l && l->up) agg += l->effective_gbps();
+              else full = false;
+            }
+            if (full && agg > cand_bw) {
+              cand = c;
+              cand_bw = agg;
+            }
+          }
+          if (!cand) break;
+          grp.push_back(cand);
+          tot += cand_bw;
+        }
+        if (static_cast<int>(grp.size()) >= k && tot > best_bw) {
+          best.clear();
+          for (auto* g : grp) best.push_back(g->uuid);
+          best_bw = tot;
+        }
+      }
+      if (static_cast<int>(best.size()) < k) {
+        first_k();
+        return 30;
+      }
+      *sel = best;
+      return static_cast<int>(50 + 50 * best_bw / (900.0 * (k * (k - 1) / 2)));
+    }
+    case TopologyPreference::SameNUMA: {
+      std::map<int, std::vector<const GpuDevice*>> groups;
+      for (auto* g : avail) groups[g->numa_node].push_back(g);
+      for (auto& kv : groups)
+        if (static_cast<int>(kv.second.size()) >= k) {
+          for (int i = 0; i < k; ++i) sel->push_back(kv.second[i]->uuid);
+          return 90;
+        }
+      first_k();
+      return 50;
+    }
+    case TopologyPreference::SamePCIeSwitch: {
+      std::map<std::string, std::vector<const GpuDevice*>> groups;
+      for (auto* g : avail) groups[g->pcie.switch_id.empty() ? "default" : g->pcie.switch_id].push_back(g);
+      for (auto& kv : groups)
+        if (static_cast<int>(kv.second.size()) >= k) {
+          for (int i = 0; i < k; ++i) sel->push_back(kv.second[i]->uuid);
+          return 80;
+        }
+      first_k();
+      return 40;
+    }
+    default:
+      first_k();
+      return 50;
+  }
+}
+
+int Scheduler::resource_score(const std::vector<const GpuDevice*>& avail,
+                              const WorkloadRequest& w) const {
+  if (avail.empty()) return 0;
+  int score = 50;
+  double free_gb = 0.0, util = 0.0;
+  for (auto* g : avail) {
+    free_gb += g->memory_free_gb();
+    util += g->util.gfx_activity;
+  }
+  util /= static_cast<double>(avail.size());
+  const double need = w.min_memory_gb * std::max(1, w.gpu_count);
+  if (free_gb >= 2 * need) score += 25;
+  else if (free_gb >= need) score += 10;
+  if (util < 30) score += 25;
+  else if (util < 60) score += 10;
+  return std::min(100, score);
+}
+
+int Scheduler::balance_score(const NodeTopology& n) const {
+  if (n.gpus.empty()) return 0;
+  double used;
+  if (cfg_.mode == ScoringMode::Compat) {
+    int allocs = 0;  // reference counts WORKLOADS on the node
+    for (const auto& kv : allocs_) allocs += kv.second.node == n.name;
+    used = allocs;
+  } else {
+    auto it = node_gpus_used_.find(n.name);
+    used = it == node_gpus_used_.end() ? 0 : it->second;
+  }
+  return std::max(0, static_cast<int>(100.0 * (1.0 - used / n.gpus.size())));
+}
+
+double Scheduler::bandwidth_of(const NodeTopology& n, const std::vector<std::string>& gpus) const {
+  double sum = 0;
+  int pairs = 0;
+  for (size_t i = 0; i < gpus.size(); ++i)
+    for (size_t j = i + 1; j < gpus.size(); ++j) {
+      const GpuDevice* a = n.gpu(gpus[i]);
+      const GpuDevice* b = n.gpu(gpus[j]);
+      if (!a || !b) continue;
+      bool up = false;
+      sum += pair_bw(*a, *b, &up);
+      ++pairs;
+    }
+  return pairs ? sum / pairs : 0.0;
+}
+
+NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w) const {
+  NodeScore s;
+  s.node = n.name;
+  if (w.partition) {
+    std::vector<std::string> gpu_of;
+    auto parts = free_partitions(n, w, &gpu_of);
+    if (static_cast<int>(parts.size()) < w.partition_count) return s;
+    // Best fit: fill GPUs that already have the most slices in use.
+    std::map<std::string, int> used_on;
+    for (const auto& g : n.gpus)
+      for (const auto& pi : g.partition.instances)
+        used_on[g.uuid] += (pi.in_use || part_owner_.count(pi.id)) ? 1 : 0;
+    std::vector<size_t> order(parts.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+      return used_on[gpu_of[a]] > used_on[gpu_of[b]];
+    });
+    for (int i = 0; i < w.partition_count; ++i) s.partitions.push_back(parts[order[i]]->id);
+    int total_slices = 0, used_slices = 0;
+    for (auto& kv : used_on) used_slices += kv.second;
+    for (const auto& g : n.gpus)
+      if (g.partition.compute == w.partition_mode) total_slices += static_cast<int>(g.partition.instances.size());
+    s.topology = 100;
+    s.resource = 50 + (total_slices ? 50 * used_slices / total_slices : 0);  // packing
+    s.balance = balance_score(n);
+  } else {
+    auto avail = free_gpus(n, w);
+    if (static_cast<int>(avail.size()) < w.gpu_count) return s;
+    bool clique = false;
+    if (cfg_.mode == ScoringMode::Compat) {
+      s.topology = topology_score_compat(n, avail, w, &s.gpus);
+      s.bandwidth_gbps = bandwidth_of(n, s.gpus);
+    } else {
+      s.topology = topology_score(n, avail, w, &s.gpus, &s.bandwidth_gbps, &clique);
+    }
+    s.resource = resource_score(avail, w);
+    s.balance = balance_score(n);
+  }
+  s.total = (s.topology * cfg_.topology_weight + s.resource * cfg_.resource_weight +
+             s.balance * cfg_.balance_weight) / 100;
+  if (std::find(w.preferred_nodes.begin(), w.preferred_nodes.end(), n.name) != w.preferred_nodes.end()) {
+    s.total += 10;
+    s.reasons.push_back("workload optimizer prefers this node");
+  }
+  int wsum = 0, wmatch = 0;
+  for (const auto& t : w.preferred_affinity) {
+    wsum += std::max(1, t.weight);
+    if (term_matches(t, n.labels)) wmatch += std::max(1, t.weight);
+  }
+  if (wsum) {
+    s.affinity = 10 * wmatch / wsum;
+    s.total += s.affinity;
+  }
+  if (s.topology >= 80) s.reasons.push_back(w.gpu_count > 1 ? "optimal xGMI connectivity" : "single GPU, best-fit placement");
+  if (s.resource >= 80) s.reasons.push_back("sufficient resources with headroom");
+  if (s.balance >= 80) s.reasons.push_back("good load distribution");
+  return s;
+}
+
+bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending) {
+  for (const auto& g : s.gpus)
+    if (gpu_owner_.count(g)) return false;
+  for (const auto& p : s.partitions)
+    if (part_owner_.count(p)) return false;
+  if (s.gpus.empty() && s.partitions.empty()) return false;
+  Allocation a;
+  a.uid = w.uid;
+  a.node = s.node;
+  a.ns = w.ns;
+  a.team = w.team;
+  a.gang = w.gang;
+  a.gpus = s.gpus;
+  a.partitions = s.partitions;
+  a.type = w.type;
+  a.priority = w.priority;
+  a.preemptible = w.preemptible;
+  a.gang_pending = gang_pending;
+  a.allocated_ns = now_ns();
+  a.bandwidth_gbps = s.bandwidth_gbps;
+  for (const auto& g : s.gpus) gpu_owner_[g] = w.uid;
+  for (const auto& p : s.partitions) part_owner_[p] = w.uid;
+  node_gpus_used_[s.node] += static_cast<int>(s.gpus.size());
+  allocs_[w.uid] = std::move(a);
+  return true;
+}
+
+void Scheduler::emit(SchedEvent e) {
+  std::lock_guard<std::mutex> lk(ev_mu_);
+  if (events_.size() >= cfg_.event_capacity) events_.pop_front();
+  events_.push_back(std::move(e));
+}
+
+std::vector<SchedEvent> Scheduler::drain_events(size_t max) {
+  std::lock_guard<std::mutex> lk(ev_mu_);
+  std::vector<SchedEvent> out;
+  size_t n = max == 0 ? events_.size() : std::min(max, events_.size());
+  for (size_t i = 0; i < n; ++i) {
+    out.push_back(std::move(events_.front()));
+    events_.pop_front();
+  }
+  return out;
+}
+
+static Decision decision_from(const Allocation& a, int score, const std::string& status) {
+  Decision d;
+  d.ok = true;
+  d.status = status;
+  d.uid = a.uid;
+  d.node = a.node;
+  d.gpus = a.gpus;
+  d.partitions = a.partitions;
+  d.score = score;
+  d.bandwidth_gbps = a.bandwidth_gbps;
+  return d;
+}
+
+Decision Scheduler::schedule(const WorkloadRequest& w) {
+  const auto t0 = std::chrono::steady_clock::now();
+  Decision d;
+  d.uid = w.uid;
+  auto snap = disc_->snapshot();
+  auto finish = [&](Decision& dd) {
+    dd.latency_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    latency_.record_ms(dd.latency_ms);
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    stats_.attempts++;
+    if (dd.ok) {
+      stats_.scheduled++;
+      if (dd.score > 0 && !dd.gpus.empty()) {
+        // topology-optimal = the chosen group's topology sub-score >= 80
+      }
+    } else {
+      stats_.failed++;
+    }
+  };
+  {
+    std::shared_lock<std::shared_mutex> lk(mu_);
+    auto it = allocs_.find(w.uid);
+    if (it != allocs_.end()) {  // idempotent re-schedule
+      d = decision_from(it->second, 0, it->second.gang_pending ? "Waiting" : "Scheduled");
+      finish(d);
+      return d;
+    }
+  }
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    std::vector<NodeScore> scores;
+    {
+      std::shared_lock<std::shared_mutex> lk(mu_);
+      for (const auto& kv : snap->nodes) {
+        std::string why = eligible(kv.second, w);
+        if (!why.empty()) {
+          d.failed_nodes[kv.first] = why;
+          continue;
+        }
+        NodeScore s = score_node(kv.second, w);
+        if (s.total > 0 && (!s.gpus.empty() || !s.partitions.empty())) scores.push_back(std::move(s));
+      }
+    }
+    std::sort(scores.begin(), scores.end(), [](const NodeScore& a, const NodeScore& b) {
+      return a.total != b.total ? a.total > b.total : a.node < b.node;
+    });
+    const int tries = std::min<int>(static_cast<int>(scores.size()), std::max(1, cfg_.max_attempts));
+    for (int i = 0; i < tries; ++i) {
+      std::unique_lock<std::shared_mutex> lk(mu_);
+      NodeScore s = scores[i];
+      const NodeTopology& n = snap->nodes.at(s.node);
+      bool stale = false;
+      for (const auto& g : s.gpus) stale |= gpu_owner_.count(g) > 0;
+      for (const auto& p : s.partitions) stale |= part_owner_.count(p) > 0;
+      if (stale) {  // lost a race: re-score this node under the write lock
+        if (!eligible(n, w).empty()) continue;
+        s = score_node(n, w);
+        if (s.gpus.empty() && s.partitions.empty()) continue;
+      }
+      const bool gang = cfg_.enable_gang && !w.gang.empty() && w.gang_size > 1;
+      if (!reserve_locked(w, s, gang)) continue;
+      d.ok = true;
+      d.status = "Scheduled";
+      d.node = s.node;
+      d.gpus = s.gpus;
+      d.partitions = s.partitions;
+      d.score = s.total;
+      d.bandwidth_gbps = s.bandwidth_gbps;
+      d.reasons = s.reasons;
+      d.failed_nodes.clear();
+      if (gang) {
+        Gang& gg = gangs_[w.gang];
+        gg.size = w.gang_size;
+        if (gg.members.empty()) gg.first_ns = now_ns();
+        gg.members.insert(w.uid);
+        if (static_cast<int>(gg.members.size()) >= gg.size) {
+          gg.ready = true;
+          for (const auto& m : gg.members) allocs_[m].gang_pending = false;
+          emit({SchedEventType::GangReady, w.gang, s.node, std::to_string(gg.size), now_ns()});
+        } else {
+          d.status = "Waiting";
+        }
+      }
+      if (s.topology >= 80) {
+        std::lock_guard<std::mutex> sl(stat_mu_);
+        stats_.topology_optimal++;
+      }
+      lk.unlock();
+      emit({SchedEventType::Scheduled, w.uid, s.node, "", now_ns()});
+      finish(d);
+      return d;
+    }
+    if (attempt == 0 && cfg_.enable_preemption && w.priority > 0) {
+      std::unique_lock<std::shared_mutex> lk(mu_);
+      if (try_preempt(w, snap, &d)) continue;
+    }
+    break;
+  }
+  d.ok = false;
+  d.status = "Unschedulable";
+  emit({SchedEventType::Failed, w.uid, "", "", now_ns()});
+  finish(d);
+  return d;
+}
+
+// Caller holds mu_ exclusively.  Picks, over all nodes, the cheapest set of
+// lower-priority preemptible allocations whose removal makes the node
+// eligible; cost = (sum of victim priorities, #victims, victim GPUs).
+bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d) {
+  struct Plan {
+    std::string node;
+    std::vector<std::string> victims;
+    std::tuple<int64_t, size_t, size_t> cost{INT64_MAX, 0, 0};
+  } best;
+  for (const auto& kv : snap->nodes) {
+    std::vector<const Allocation*> cands;
+    for (const auto& a : allocs_)
+      if (a.second.node == kv.first && a.second.preemptible && a.second.priority < w.priority)
+        cands.push_back(&a.second);
+    if (cands.empty()) continue;
+    std::sort(cands.begin(), cands.end(), [](const Allocation* a, const Allocation* b) {
+      if (a->priority != b->priority) return a->priority < b->priority;
+      return a->allocated_ns > b->allocated_ns;  // youngest first: least work lost
+    });
+    // Temporarily hide victims one by one until the node becomes eligible.
+    std::vector<std::string> victims;
+    std::vector<std::pair<std::string, std::string>> hidden_g, hidden_p;
+    int64_t prio = 0;
+    size_t ngpu = 0;
+    bool ok = false;
+    for (const Allocation* a : cands) {
+      victims.push_back(a->uid);
+      prio += a->priority;
+      ngpu += a->gpus.size() + a->partitions.size();
+      for (const auto& g : a->gpus) {
+        hidden_g.emplace_back(g, gpu_owner_[g]);
+        gpu_owner_.erase(g);
+      }
+      for (const auto& p : a->partitions) {
+        hidden_p.emplace_back(p, part_owner_[p]);
+        part_owner_.erase(p);
+      }
+      if (eligible(kv.second, w).empty()) {
+        ok = true;
+        break;
+      }
+    }
+    for (auto& h : hidden_g) gpu_owner_[h.first] = h.second;
+    for (auto& h : hidden_p) part_owner_[h.first] = h.second;
+    if (!ok) continue;
+    std::tuple<int64_t, size_t, size_t> cost{prio, victims.size(), ngpu};
+    if (cost < best.cost) {
+      best.node = kv.first;
+      best.victims = victims;
+      best.cost = cost;
+    }
+  }
+  if (best.node.empty()) return false;
+  for (const auto& uid : best.victims) {
+    auto it = allocs_.find(uid);
+    if (it == allocs_.end()) continue;
+    for (const auto& g : it->second.gpus) gpu_owner_.erase(g);
+    for (const auto& p : it->second.partitions) part_owner_.erase(p);
+    node_gpus_used_[it->second.node] -= static_cast<int>(it->second.gpus.size());
+    if (!it->second.gang.empty()) gangs_[it->second.gang].members.erase(uid);
+    allocs_.erase(it);
+    d->preempted.push_back(uid);
+    emit({SchedEventType::Preempted, uid, best.node, "by " + w.uid, now_ns()});
+  }
+  std::lock_guard<std::mutex> sl(stat_mu_);
+  stats_.preemptions += best.victims.size();
+  return true;
+}
+
+std::vector<Decision> Scheduler::schedule_gang(const std::vector<WorkloadRequest>& members) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<Decision> out;
+  auto snap = disc_->snapshot();
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::vector<std::string> placed;
+  bool ok = true;
+  for (const auto& w : members) {
+    Decision d;
+    d.uid = w.uid;
+    NodeScore best;
+    for (const auto& kv : snap->nodes) {
+      std::string why = eligible(kv.second, w);
+      if (!why.empty()) {
+        d.failed_nodes[kv.first] = why;
+        continue;
+      }
+      NodeScore s = score_node(kv.second, w);
+      if ((s.gpus.empty() && s.partitions.empty()) || s.total <= 0) continue;
+      if (s.total > best.total || (s.total == best.total && s.node < best.node)) best = s;
+    }
+    WorkloadRequest wm = w;
+    wm.gang.clear();  // the whole gang is placed atomically here
+    if (best.node.empty() || !reserve_locked(wm, best, false)) {
+      ok = false;
+      d.status = "Unschedulable";
+      out.push_back(d);
+      break;
+    }
+    allocs_[w.uid].gang = w.gang;
+    placed.push_back(w.uid);
+    d.ok = true;
+    d.status = "Scheduled";
+    d.node = best.node;
+    d.gpus = best.gpus;
+    d.partitions = best.partitions;
+    d.score = best.total;
+    d.bandwidth_gbps = best.bandwidth_gbps;
+    d.reasons = best.reasons;
+    out.push_back(d);
+  }
+  if (!ok) {  // roll back: all or nothing
+    for (const auto& uid : placed) {
+      auto it = allocs_.find(uid);
+      for (const auto& g : it->second.gpus) gpu_owner_.erase(g);
+      for (const auto& p : it->second.partitions) part_owner_.erase(p);
+      node_gpus_used_[it->second.node] -= static_cast<int>(it->second.gpus.size());
+      allocs_.erase(it);
+    }
+    for (auto& d : out) {
+      d.ok = false;
+      d.status = "Unschedulable";
+      d.gpus.clear();
+      d.partitions.clear();
+    }
+  }
+  lk.unlock();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  latency_.record_ms(ms);
+  std::lock_guard<std::mutex> sl(stat_mu_);
+  stats_.attempts += members.size();
+  if (ok) stats_.scheduled += members.size();
+  else stats_.failed += members.size();
+  return out;
+}
+
+std::map<std::string, std::string> Scheduler::filter(const WorkloadRequest& w,
+                                                     const std::vector<std::string>& nodes,
+                                                     std::vector<std::string>* passed) {
+  std::map<std::string, std::string> failed;
+  auto snap = disc_->snapshot();
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  auto mine = allocs_.find(w.uid);
+  for (const auto& name : nodes) {
+    auto it = snap->nodes.find(name);
+    if (it == snap->nodes.end()) {
+      failed[name] = "node not managed by kgwe (no MI355X topology)";
+      continue;
+    }
+    if (mine != allocs_.end()) {  // already reserved (gang member / retry): only that node
+      if (mine->second.node == name) passed->push_back(name);
+      else failed[name] = "workload already reserved on " + mine->second.node;
+      continue;
+    }
+    std::string why = eligible(it->second, w);
+    if (why.empty()) passed->push_back(name);
+    else failed[name] = why;
+  }
+  return failed;
+}
+
+std::vector<NodeScore> Scheduler::prioritize(const WorkloadRequest& w,
+                                             const std::vector<std::string>& nodes) {
+  std::vector<NodeScore> out;
+  auto snap = disc_->snapshot();
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  for (const auto& name : nodes) {
+    auto it = snap->nodes.find(name);
+    NodeScore s;
+    s.node = name;
+    if (it != snap->nodes.end() && eligible(it->second, w).empty()) s = score_node(it->second, w);
+    s.node = name;
+    out.push_back(std::move(s));
+  }
+  return out;
+}
+
+Decision Scheduler::bind(const WorkloadRequest& w, const std::string& node) {
+  const auto t0 = std::chrono::steady_clock::now();
+  Decision d;
+  d.uid = w.uid;
+  auto snap = disc_->snapshot();
+  auto it = snap->nodes.find(node);
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  auto mine = allocs_.find(w.uid);
+  if (mine != allocs_.end()) {
+    if (mine->second.node != node) {
+      d.status = "Unschedulable";
+      d.failed_nodes[node] = "already reserved on " + mine->second.node;
+      return d;
+    }
+    d = decision_from(mine->second, 0, mine->second.gang_pending ? "Waiting" : "Scheduled");
+    return d;
+  }
+  if (it == snap->nodes.end()) {
+    d.status = "Unschedulable";
+    d.failed_nodes[node] = "unknown node";
+    return d;
+  }
+  std::string why = eligible(it->second, w);
+  NodeScore s;
+  if (why.empty()) s = score_node(it->second, w);
+  const bool gang = cfg_.enable_gang && !w.gang.empty() && w.gang_size > 1;
+  if (!why.empty() || !reserve_locked(w, s, gang)) {
+    d.status = "Unschedulable";
+    d.failed_nodes[node] = why.empty() ? "reservation conflict" : why;
+    lk.unlock();
+    std::lock_guard<std::mutex> sl(stat_mu_);
+    stats_.attempts++;
+    stats_.failed++;
+    return d;
+  }
+  d.ok = true;
+  d.status = "Scheduled";
+  d.node = node;
+  d.gpus = s.gpus;
+  d.partitions = s.partitions;
+  d.score = s.total;
+  d.bandwidth_gbps = s.bandwidth_gbps;
+  d.reasons = s.reasons;
+  if (gang) {
+    Gang& gg = gangs_[w.gang];
+    gg.size = w.gang_size;
+    if (gg.members.empty()) gg.first_ns = now_ns();
+    gg.members.insert(w.uid);
+    if (static_cast<int>(gg.members.size()) >= gg.size) {
+      gg.ready = true;
+      for (const auto& m : gg.members) allocs_[m].gang_pending = false;
+      emit({SchedEventType::GangReady, w.gang, node, std::to_string(gg.size), now_ns()});
+    } else {
+      d.status = "Waiting";
+    }
+  }
+  const bool optimal = s.topology >= 80;
+  lk.unlock();
+  emit({SchedEventType::Scheduled, w.uid, node, "", now_ns()});
+  d.latency_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::lock_guard<std::mutex> sl(stat_mu_);
+  stats_.attempts++;
+  stats_.scheduled++;
+  if (optimal) stats_.topology_optimal++;
+  return d;
+}
+
+std::string Scheduler::permit(const std::string& uid) {
+  expire_gangs();
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  auto it = allocs_.find(uid);
+  if (it == allocs_.end()) return "Reject";
+  if (it->second.gang.empty() || !it->second.gang_pending) return "Allow";
+  auto g = gangs_.find(it->second.gang);
+  if (g != gangs_.end() && g->second.ready) return "Allow";
+  return "Wait";
+}
+
+void Scheduler::expire_gangs() {
+  std::vector<std::string> expired;
+  {
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    const int64_t now = now_ns();
+    for (auto it = gangs_.begin(); it != gangs_.end();) {
+      Gang& g = it->second;
+      if (!g.ready && !g.members.empty() &&
+          now - g.first_ns > static_cast<int64_t>(cfg_.gang_timeout_ms) * 1000000) {
+        for (const auto& uid : g.members) {
+          auto a = allocs_.find(uid);
+          if (a == allocs_.end()) continue;
+          for (const auto& gp : a->second.gpus) gpu_owner_.erase(gp);
+          for (const auto& p : a->second.partitions) part_owner_.erase(p);
+          node_gpus_used_[a->second.node] -= static_cast<int>(a->second.gpus.size());
+          allocs_.erase(a);
+        }
+        expired.push_back(it->first);
+        it = gangs_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (const auto& g : expired) emit({SchedEventType::GangTimeout, g, "", "", now_ns()});
+  if (!expired.empty()) {
+    std::lock_guard<std::mutex> sl(stat_mu_);
+    stats_.gang_timeouts += expired.size();
+  }
+}
+
+bool Scheduler::release(const std::string& uid) {
+  std::string node;
+  {
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    auto it = allocs_.find(uid);
+    if (it == allocs_.end()) return false;
+    node = it->second.node;
+    for (const auto& g : it->second.gpus) gpu_owner_.erase(g);
+    for (const auto& p : it->second.partitions) part_owner_.erase(p);
+    node_gpus_used_[node] -= static_cast<int>(it->second.gpus.size());
+    if (!it->second.gang.empty()) {
+      auto g = gangs_.find(it->second.gang);
+      if (g != gangs_.end()) {
+        g->second.members.erase(uid);
+        if (g->second.members.empty()) gangs_.erase(g);
+      }
+    }
+    allocs_.erase(it);
+  }
+  emit({SchedEventType::Released, uid, node, "", now_ns()});
+  std::lock_guard<std::mutex> sl(stat_mu_);
+  stats_.releases++;
+  return true;
+}
+
+bool Scheduler::restore(const Allocation& a) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  if (allocs_.count(a.uid)) return false;
+  for (const auto& g : a.gpus)
+    if (gpu_owner_.count(g)) return false;
+  for (const auto& p : a.partitions)
+    if (part_owner_.count(p)) return false;
+  for (const auto& g : a.gpus) gpu_owner_[g] = a.uid;
+  for (const auto& p : a.partitions) part_owner_[p] = a.uid;
+  node_gpus_used_[a.node] += static_cast<int>(a.gpus.size());
+  Allocation c = a;
+  if (!c.allocated_ns) c.allocated_ns = now_ns();
+  allocs_[a.uid] = c;
+  return true;
+}
+
+std::vector<Allocation> Scheduler::allocations() const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::vector<Allocation> out;
+  out.reserve(allocs_.size());
+  for (const auto& kv : allocs_) out.push_back(kv.second);
+  std::sort(out.begin(), out.end(), [](const Allocation& a, const Allocation& b) { return a.uid < b.uid; });
+  return out;
+}
+
+bool Scheduler::allocation(const std::string& uid, Allocation* out) const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  auto it = allocs_.find(uid);
+  if (it == allocs_.end()) return false;
+  if (out) *out = it->second;
+  return true;
+}
+
+SchedulerMetrics Scheduler::metrics() const {
+  SchedulerMetrics m;
+  {
+    std::lock_guard<std::mutex> lk(stat_mu_);
+    m = stats_;
+  }
+  m.avg_latency_ms = latency_.mean_ms();
+  m.p50_ms = latency_.quantile_ms(0.50);
+  m.p90_ms = latency_.quantile_ms(0.90);
+  m.p99_ms = latency_.quantile_ms(0.99);
+  m.max_ms = latency_.max_ms();
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  m.active_allocations = allocs_.size();
+  m.allocated_gpus = gpu_owner_.size();
+  m.allocated_partitions = part_owner_.size();
+  return m;
+}
+
+}  // namespace kgwe
