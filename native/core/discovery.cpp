@@ -81,6 +81,18 @@ void DiscoveryService::refresh() {
   publish(next, snapshot());
 }
 
+bool DiscoveryService::refresh_node(const std::string& name) {
+  std::shared_ptr<Hal> h = hal(name);
+  if (!h) return false;
+  NodeTopology n = h->discover(name);
+  std::lock_guard<std::mutex> lk(publish_mu_);
+  auto prev = snapshot();
+  auto next = std::make_shared<ClusterTopology>(*prev);
+  next->nodes[name] = std::move(n);
+  publish(next, prev);
+  return true;
+}
+
 void DiscoveryService::refresh_telemetry() {
   std::vector<std::pair<std::string, std::shared_ptr<Hal>>> hs;
   {

@@ -69,6 +69,8 @@ class DiscoveryService {
 
   // Full refresh: discover every HAL-backed node off-lock, then publish.
   void refresh();
+  // Re-discover one HAL-backed node (e.g. after a partition switch).
+  bool refresh_node(const std::string& name);
   // Telemetry-only refresh of the HAL-backed nodes (cheap, periodic).
   void refresh_telemetry();
   void start();

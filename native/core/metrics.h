@@ -1,0 +1,64 @@
+// Prometheus metric registry + text exposition (format 0.0.4).
+//
+// Reference: src/monitoring/prometheus_exporter.go (primitives :135-238,
+// 27 kgwe_* families :256-411, exposition :542-629).  Fixed: label SETS are
+// kept per series (the reference collapsed them into one composite
+// `label="node/uuid"`, :614-616, breaking the Grafana `node=~"$node"` filter),
+// histogram `le` values are formatted exactly (not "%f", :598), every family is
+// exposed (WorkloadDuration was never written), and the recorders are actually
+// called by the scheduler / cost engine / agent.
+#pragma once
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace kgwe {
+
+enum class MetricType { Counter, Gauge, Histogram };
+
+class MetricRegistry {
+ public:
+  using Labels = std::vector<std::string>;  // values, in the family's label order
+
+  void declare(const std::string& name, MetricType type, const std::string& help,
+               const std::vector<std::string>& label_names,
+               const std::vector<double>& buckets = {});
+  void set(const std::string& name, const Labels& lv, double v);
+  void add(const std::string& name, const Labels& lv, double v = 1.0);
+  void observe(const std::string& name, const Labels& lv, double v);
+  void remove(const std::string& name, const Labels& lv);
+  void clear(const std::string& name);  // drop all series of a family
+  double value(const std::string& name, const Labels& lv) const;
+  bool has(const std::string& name) const;
+  std::string expose() const;
+  std::vector<std::string> families() const;
+
+  // The kgwe_* families (reference names kept; NVLink -> xGMI, MIG -> partition,
+  // plus xGMI link status, partition mode and gfx activity gauges).
+  void declare_kgwe_families();
+
+ private:
+  struct Series {
+    double value = 0.0;
+    std::vector<double> bucket_counts;  // histogram: per-bucket (non-cumulative)
+    double sum = 0.0;
+    uint64_t count = 0;
+  };
+  struct Family {
+    MetricType type;
+    std::string help;
+    std::vector<std::string> labels;
+    std::vector<double> buckets;
+    std::map<Labels, Series> series;
+  };
+  Family* find(const std::string& name);
+  mutable std::mutex mu_;
+  std::map<std::string, Family> fams_;
+};
+
+std::string prom_escape(const std::string& v);
+std::string prom_number(double v);
+
+}  // namespace kgwe

@@ -1,0 +1,504 @@
+#include "partition.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace kgwe {
+
+const char* to_string(OpState s) {
+  switch (s) {
+    case OpState::Pending: return "Pending";
+    case OpState::Draining: return "Draining";
+    case OpState::Switching: return "Switching";
+    case OpState::Completed: return "Completed";
+    case OpState::Failed: return "Failed";
+  }
+  return "Unknown";
+}
+
+// ---------------------------------------------------------------------------
+// strategies
+// ---------------------------------------------------------------------------
+std::string validate_strategy(const PartitionStrategy& s) {
+  if (s.name.empty()) return "strategy name is required";
+  if (s.distribution.empty()) return "profileDistribution must not be empty";
+  double sum = 0.0;
+  for (const auto& kv : s.distribution) {
+    if (kv.first == ComputePartition::TPX) return "TPX is not a valid MI355X mode (8 XCDs)";
+    if (kv.second < 0.0 || kv.second > 1.0) return "distribution fractions must be in [0, 1]";
+    sum += kv.second;
+  }
+  if (sum > 1.01) return "distribution sums to more than 1.0";
+  if (s.memory == MemoryPartition::NPS4 || s.memory == MemoryPartition::NPS8)
+    return "MI355X supports NPS1 and NPS2 memory modes";
+  if (s.min_utilization < 0.0 || s.min_utilization > 1.0) return "minUtilizationThreshold must be in [0, 1]";
+  if (s.rebalance_interval_s < 0) return "rebalanceInterval must be >= 0";
+  return "";
+}
+
+static int parse_duration_s(const std::string& d, int dflt) {
+  if (d.empty()) return dflt;
+  try {
+    size_t pos = 0;
+    double v = std::stod(d, &pos);
+    std::string unit = d.substr(pos);
+    if (unit == "s" || unit.empty()) return static_cast<int>(v);
+    if (unit == "m") return static_cast<int>(v * 60);
+    if (unit == "h") return static_cast<int>(v * 3600);
+  } catch (...) {
+  }
+  return dflt;
+}
+
+PartitionStrategy strategy_from_json(const Json& in) {
+  PartitionStrategy s;
+  const Json& meta = in.get("metadata");
+  const Json& spec = in.has("spec") ? in.get("spec") : in;
+  s.name = meta.get("name").str(in.get("name").str());
+  for (const auto& kv : spec.get("nodeSelector").fields()) s.node_selector[kv.first] = kv.second.str();
+  const Json& gs = spec.get("gpuSelector");
+  s.gpu_model = gs.get("model").str();
+  s.min_memory_gb = gs.get("minMemoryGB").as_number(0.0);
+  for (const auto& kv : spec.get("profileDistribution").fields())
+    s.distribution[compute_partition_from(kv.first)] += kv.second.as_number(0.0);
+  s.memory = memory_partition_from(spec.get("memoryPartition").str("NPS1"));
+  s.allow_dynamic = spec.get("allowDynamicReconfig").as_bool(true);
+  s.rebalance_interval_s = parse_duration_s(spec.get("rebalanceInterval").str("5m"), 300);
+  s.min_utilization = spec.get("minUtilizationThreshold").as_number(0.3);
+  s.priority = static_cast<int>(spec.get("priority").as_int(0));
+  return s;
+}
+
+Json to_json(const PartitionStrategy& s) {
+  Json j = Json::object();
+  j["name"] = s.name;
+  Json d = Json::object();
+  for (const auto& kv : s.distribution) d[to_string(kv.first)] = kv.second;
+  j["profileDistribution"] = d;
+  j["memoryPartition"] = to_string(s.memory);
+  j["allowDynamicReconfig"] = s.allow_dynamic;
+  j["rebalanceIntervalSeconds"] = s.rebalance_interval_s;
+  j["minUtilizationThreshold"] = s.min_utilization;
+  j["priority"] = s.priority;
+  return j;
+}
+
+Json to_json(const PartitionOp& op) {
+  Json j = Json::object();
+  j["id"] = op.id;
+  j["node"] = op.node;
+  j["gpu"] = op.gpu;
+  j["from"] = to_string(op.from);
+  j["to"] = to_string(op.to);
+  j["state"] = to_string(op.state);
+  j["reason"] = op.reason;
+  j["error"] = op.error;
+  j["dry_run"] = op.dry_run;
+  return j;
+}
+
+// ---------------------------------------------------------------------------
+// controller
+// ---------------------------------------------------------------------------
+PartitionController::PartitionController(std::shared_ptr<DiscoveryService> disc,
+                                         std::shared_ptr<Scheduler> sched, bool dry_run)
+    : disc_(std::move(disc)), sched_(std::move(sched)), dry_run_(dry_run) {}
+
+std::string PartitionController::register_strategy(const PartitionStrategy& s) {
+  std::string err = validate_strategy(s);
+  if (!err.empty()) return err;
+  std::lock_guard<std::mutex> lk(mu_);
+  strategies_[s.name] = s;
+  return "";
+}
+
+bool PartitionController::remove_strategy(const std::string& name) {
+  std::lock_guard<std::mutex> lk(mu_);
+  return strategies_.erase(name) > 0;
+}
+
+std::vector<PartitionStrategy> PartitionController::strategies() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<PartitionStrategy> out;
+  for (const auto& kv : strategies_) out.push_back(kv.second);
+  return out;
+}
+
+bool PartitionController::gpu_idle(const GpuDevice& g) const {
+  if (!g.healthy() || g.partition.switching) return false;
+  if (sched_ && sched_->gpu_busy(g)) return false;
+  for (const auto& pi : g.partition.instances)
+    if (pi.in_use) return false;
+  return g.util.gfx_activity < 5.0;
+}
+
+int PartitionController::free_slices(const ClusterTopology& c, ComputePartition mode) const {
+  int n = 0;
+  for (const auto& kv : c.nodes)
+    for (const auto& g : kv.second.gpus) {
+      if (g.partition.compute != mode || !g.healthy() || g.partition.switching) continue;
+      if (sched_ && g.partition.compute == ComputePartition::SPX && sched_->gpu_busy(g)) continue;
+      for (const auto& pi : g.partition.instances) {
+        if (pi.in_use) continue;
+        bool owned = false;
+        if (sched_) {
+          // A slice is owned when the ledger holds it; gpu_busy() is per GPU,
+          // so check slice ownership through the allocation list.
+          for (const auto& a : sched_->allocations())
+            if (std::find(a.partitions.begin(), a.partitions.end(), pi.id) != a.partitions.end()) owned = true;
+        }
+        n += owned ? 0 : 1;
+      }
+    }
+  return n;
+}
+
+PartitionOp PartitionController::execute(const std::string& node, const GpuDevice& g,
+                                         ComputePartition to, const std::string& reason,
+                                         bool plan_only) {
+  PartitionOp op;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    op.id = "op-" + std::to_string(next_op_++);
+  }
+  op.node = node;
+  op.gpu = g.uuid;
+  op.from = g.partition.compute;
+  op.to = to;
+  op.mem_to = g.partition.memory;
+  op.reason = reason;
+  op.dry_run = dry_run_ || plan_only;
+  op.created_ns = now_ns();
+  if (!plan_only) {
+    // Drain: the GPU was chosen idle; re-verify right before switching.
+    op.state = OpState::Draining;
+    if (!gpu_idle(g)) {
+      op.state = OpState::Failed;
+      op.error = "gpu no longer idle";
+    } else if (dry_run_) {
+      op.state = OpState::Completed;
+    } else {
+      op.state = OpState::Switching;
+      auto hal = disc_->hal(node);
+      std::string err = hal ? hal->set_compute_partition(g.uuid, to) : "no HAL for node " + node;
+      if (err.empty()) {
+        disc_->refresh_node(node);  // re-advertise the new slices
+        op.state = OpState::Completed;
+      } else {
+        op.state = OpState::Failed;
+        op.error = err;
+      }
+    }
+    op.finished_ns = now_ns();
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  ops_.push_back(op);
+  if (ops_.size() > 4096) ops_.erase(ops_.begin(), ops_.begin() + 1024);
+  return op;
+}
+
+std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition mode, int count,
+                                                              bool plan_only) {
+  std::vector<PartitionOp> out;
+  auto snap = disc_->snapshot();
+  int have = free_slices(*snap, mode);
+  if (have >= count) return out;
+  const int per_gpu = partition_count(mode);
+  // Candidate idle GPUs in a different mode; prefer nodes already running the
+  // target mode (consolidation), then nodes with the fewest idle GPUs (keep
+  // whole idle nodes intact for large training jobs), then SPX sources.
+  struct Cand {
+    std::string node;
+    const GpuDevice* g;
+    int node_has_mode, node_idle;
+  };
+  std::vector<Cand> cands;
+  for (const auto& kv : snap->nodes) {
+    int has_mode = 0, idle = 0;
+    for (const auto& g : kv.second.gpus) {
+      has_mode += g.partition.compute == mode;
+      idle += gpu_idle(g);
+    }
+    for (const auto& g : kv.second.gpus)
+      if (g.partition.compute != mode && gpu_idle(g)) cands.push_back({kv.first, &g, has_mode, idle});
+  }
+  std::stable_sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+    if (a.node_has_mode != b.node_has_mode) return a.node_has_mode > b.node_has_mode;
+    if (a.node_idle != b.node_idle) return a.node_idle < b.node_idle;
+    const bool as = a.g->partition.compute == ComputePartition::SPX;
+    const bool bs = b.g->partition.compute == ComputePartition::SPX;
+    if (as != bs) return as;
+    return a.g->index < b.g->index;
+  });
+  for (const auto& c : cands) {
+    if (have >= count) break;
+    PartitionOp op = execute(c.node, *c.g, mode,
+                             "capacity: need " + std::to_string(count) + " " + to_string(mode) +
+                                 " slices, have " + std::to_string(have),
+                             plan_only);
+    out.push_back(op);
+    if (op.state != OpState::Failed) have += per_gpu;
+  }
+  return out;
+}
+
+std::vector<PartitionOp> PartitionController::rebalance(const std::string& name, bool plan_only) {
+  std::vector<PartitionOp> out;
+  PartitionStrategy st;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = strategies_.find(name);
+    if (it == strategies_.end()) return out;
+    st = it->second;
+  }
+  if (!st.allow_dynamic) return out;
+  auto snap = disc_->snapshot();
+  // Matching GPUs.
+  std::vector<std::pair<std::string, const GpuDevice*>> match;
+  for (const auto& kv : snap->nodes) {
+    bool ok = true;
+    for (const auto& sel : st.node_selector) {
+      auto l = kv.second.labels.find(sel.first);
+      ok &= l != kv.second.labels.end() && l->second == sel.second;
+    }
+    if (!ok) continue;
+    for (const auto& g : kv.second.gpus) {
+      if (!st.gpu_model.empty() && g.model.find(st.gpu_model) == std::string::npos) continue;
+      if (g.memory_total_gb < st.min_memory_gb) continue;
+      match.emplace_back(kv.first, &g);
+    }
+  }
+  if (match.empty()) return out;
+  const int total = static_cast<int>(match.size());
+  std::map<ComputePartition, int> want, have;
+  int assigned = 0;
+  for (const auto& kv : st.distribution) {
+    want[kv.first] = static_cast<int>(std::floor(kv.second * total + 1e-9));
+    assigned += want[kv.first];
+  }
+  // Remainder stays / goes to SPX.
+  want[ComputePartition::SPX] += total - assigned;
+  for (const auto& m : match) have[m.second->partition.compute]++;
+  // Idle GPUs of over-represented modes are converted to under-represented ones.
+  for (const auto& m : match) {
+    const ComputePartition cur = m.second->partition.compute;
+    if (have[cur] <= want[cur] || !gpu_idle(*m.second)) continue;
+    ComputePartition target = cur;
+    int deficit = 0;
+    for (const auto& kv : want) {
+      int d = kv.second - have[kv.first];
+      if (d > deficit) {
+        deficit = d;
+        target = kv.first;
+      }
+    }
+    if (target == cur) break;
+    PartitionOp op = execute(m.first, *m.second, target, "rebalance strategy " + st.name, plan_only);
+    out.push_back(op);
+    if (op.state != OpState::Failed) {
+      have[cur]--;
+      have[target]++;
+    }
+  }
+  return out;
+}
+
+std::vector<PartitionOp> PartitionController::reclaim_idle(bool plan_only) {
+  std::vector<PartitionOp> out;
+  auto snap = disc_->snapshot();
+  for (const auto& kv : snap->nodes)
+    for (const auto& g : kv.second.gpus)
+      if (g.partition.compute != ComputePartition::SPX && gpu_idle(g))
+        out.push_back(execute(kv.first, g, ComputePartition::SPX, "reclaim idle partitioned GPU", plan_only));
+  return out;
+}
+
+std::vector<PartitionOp> PartitionController::operations() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return ops_;
+}
+
+PartitionMetrics PartitionController::metrics() const {
+  PartitionMetrics m;
+  auto snap = disc_->snapshot();
+  std::vector<Allocation> allocs;
+  if (sched_) allocs = sched_->allocations();
+  std::set<std::string> owned;
+  for (const auto& a : allocs)
+    for (const auto& p : a.partitions) owned.insert(p);
+  int slices = 0, used = 0;
+  for (const auto& kv : snap->nodes)
+    for (const auto& g : kv.second.gpus) {
+      auto& md = m.modes[to_string(g.partition.compute)];
+      md.gpus++;
+      md.slices += static_cast<int>(g.partition.instances.size());
+      for (const auto& pi : g.partition.instances) {
+        const bool u = pi.in_use || owned.count(pi.id);
+        md.slices_in_use += u;
+        if (g.partition.compute != ComputePartition::SPX) {
+          slices++;
+          used += u;
+        }
+      }
+    }
+  m.slice_utilization = slices ? static_cast<double>(used) / slices : 0.0;
+  std::lock_guard<std::mutex> lk(mu_);
+  m.ops_total = static_cast<int>(ops_.size());
+  for (const auto& op : ops_) {
+    m.ops_failed += op.state == OpState::Failed;
+    m.ops_pending += op.state == OpState::Pending || op.state == OpState::Draining ||
+                     op.state == OpState::Switching;
+  }
+  return m;
+}
+
+// ---------------------------------------------------------------------------
+// sharing
+// ---------------------------------------------------------------------------
+const char* to_string(SharingMethod m) {
+  switch (m) {
+    case SharingMethod::None: return "None";
+    case SharingMethod::Partition: return "Partition";
+    case SharingMethod::CoLocate: return "CoLocate";
+    case SharingMethod::TimeSlice: return "TimeSlice";
+  }
+  return "None";
+}
+
+SharingMethod sharing_method_from(const std::string& s) {
+  if (s == "Partition" || s == "MIG") return SharingMethod::Partition;
+  if (s == "CoLocate" || s == "MPS") return SharingMethod::CoLocate;
+  if (s == "TimeSlice") return SharingMethod::TimeSlice;
+  return SharingMethod::None;
+}
+
+Json to_json(const SharingAllocation& a) {
+  Json j = Json::object();
+  j["uid"] = a.uid;
+  j["node"] = a.node;
+  j["gpu"] = a.gpu;
+  j["method"] = to_string(a.method);
+  j["cu_begin"] = a.cu_begin;
+  j["cu_end"] = a.cu_end;
+  j["memory_gb"] = a.memory_gb;
+  Json env = Json::object();
+  for (const auto& kv : a.env) env[kv.first] = kv.second;
+  j["env"] = env;
+  return j;
+}
+
+SharingManager::SharingManager(std::shared_ptr<DiscoveryService> disc, SharingPolicy policy)
+    : disc_(std::move(disc)), policy_(std::move(policy)) {}
+
+SharingMethod SharingManager::decide(const SharingRequest& r) const {
+  auto it = policy_.by_type.find(r.type);
+  if (it != policy_.by_type.end()) return it->second;
+  if (r.require_isolation) return SharingMethod::Partition;
+  if (r.prefer_partition) return SharingMethod::Partition;
+  return SharingMethod::CoLocate;
+}
+
+int SharingManager::clients_on(const std::string& gpu) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  int n = 0;
+  for (const auto& kv : allocs_) n += kv.second.gpu == gpu;
+  return n;
+}
+
+SharingAllocation SharingManager::allocate(const SharingRequest& r, std::string* error) {
+  SharingAllocation a;
+  a.uid = r.uid;
+  a.method = decide(r);
+  a.node = r.node;
+  a.gpu = r.gpu;
+  if (a.method == SharingMethod::Partition) {
+    a.env["KGWE_SHARING"] = "Partition";
+    a.env["KGWE_PARTITION_MODE"] = to_string(r.partition_mode);
+    return a;
+  }
+  GpuDevice g;
+  if (!disc_->gpu(r.gpu, &g)) {
+    *error = "unknown gpu " + r.gpu;
+    return a;
+  }
+  a.gpu_index = g.index;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (allocs_.count(r.uid)) {
+    *error = "already allocated: " + r.uid;
+    return a;
+  }
+  int clients = 0;
+  std::vector<std::pair<int, int>> used;
+  for (const auto& kv : allocs_)
+    if (kv.second.gpu == r.gpu) {
+      ++clients;
+      if (kv.second.method == SharingMethod::CoLocate) used.emplace_back(kv.second.cu_begin, kv.second.cu_end);
+    }
+  if (a.method == SharingMethod::TimeSlice) {
+    if (clients >= policy_.max_timeslice_replicas) {
+      *error = "time-slice replicas exhausted on " + r.gpu;
+      return a;
+    }
+    a.env["KGWE_SHARING"] = "TimeSlice";
+  } else {
+    if (clients >= policy_.max_clients_per_gpu) {
+      *error = "co-location client limit reached on " + r.gpu;
+      return a;
+    }
+    const double pct = r.cu_percent > 0 ? r.cu_percent : policy_.default_cu_percent;
+    int want = std::max(1, static_cast<int>(std::lround(g.cu_count * pct / 100.0)));
+    // Round to whole XCDs when possible (32 CUs share one L2).
+    const int per_xcd = g.xcd_count > 0 ? g.cu_count / g.xcd_count : g.cu_count;
+    if (want >= per_xcd) want = (want + per_xcd - 1) / per_xcd * per_xcd;
+    std::sort(used.begin(), used.end());
+    int start = 0, found = -1;
+    for (const auto& u : used) {
+      if (u.first - start >= want) {
+        found = start;
+        break;
+      }
+      start = std::max(start, u.second);
+    }
+    if (found < 0 && g.cu_count - start >= want) found = start;
+    if (found < 0) {
+      *error = "not enough free compute units on " + r.gpu;
+      return a;
+    }
+    double mem_used = 0.0;
+    for (const auto& kv : allocs_)
+      if (kv.second.gpu == r.gpu) mem_used += kv.second.memory_gb;
+    if (r.memory_gb > 0 && mem_used + r.memory_gb > g.memory_free_gb() + 1e-9) {
+      *error = "memory cap exceeds free HBM on " + r.gpu;
+      return a;
+    }
+    a.cu_begin = found;
+    a.cu_end = found + want;
+    a.memory_gb = r.memory_gb;
+    a.env["KGWE_SHARING"] = "CoLocate";
+    // ROCm CU masking: device-local index : CU list (HSA_CU_MASK syntax).
+    a.env["HSA_CU_MASK"] = "0:" + std::to_string(a.cu_begin) + "-" + std::to_string(a.cu_end - 1);
+    if (r.memory_gb > 0) {
+      char buf[32];
+      std::snprintf(buf, sizeof buf, "%.3f", r.memory_gb / g.memory_total_gb);
+      a.env["KGWE_GPU_MEMORY_FRACTION"] = buf;
+    }
+  }
+  a.env["HIP_VISIBLE_DEVICES"] = std::to_string(g.index);
+  a.env["ROCR_VISIBLE_DEVICES"] = std::to_string(g.index);
+  allocs_[r.uid] = a;
+  return a;
+}
+
+bool SharingManager::release(const std::string& uid) {
+  std::lock_guard<std::mutex> lk(mu_);
+  return allocs_.erase(uid) > 0;
+}
+
+std::vector<SharingAllocation> SharingManager::allocations() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<SharingAllocation> out;
+  for (const auto& kv : allocs_) out.push_back(kv.second);
+  return out;
+}
+
+}  // namespace kgwe

@@ -1,0 +1,166 @@
+// MI355X compute/memory-partition controller (replaces the reference's MIG
+// controller, src/sharing/mig_controller.go:16-542).
+//
+// MI355X partitions are HOMOGENEOUS per GPU: a compute mode (SPX = 1 x 256
+// CUs, DPX = 2 x 128, QPX = 4 x 64, CPX = 8 x 32, one slice per XCD) applies
+// to the whole device, a mode switch needs the GPU idle, and the memory mode
+// (NPS1 / NPS2) constrains which compute modes are valid.  So unlike MIG's
+// per-slot profiles, the planner reasons at GPU-mode granularity:
+//   * ensure_capacity(mode, n): free slices of `mode` first (best fit), then
+//     convert idle SPX GPUs, preferring nodes that already run that mode
+//     (consolidation) — drain -> switch -> re-advertise;
+//   * strategies (PartitionStrategy CRD, the MIGStrategy analogue,
+//     gpuworkload-crd.yaml:248-366): validated mode distribution, rebalanced
+//     onto idle GPUs only;
+//   * every reconfiguration is an Operation with a state machine
+//     (Pending -> Draining -> Switching -> Completed | Failed), actuated
+//     through the node's HAL (amd-smi set_gpu_compute_partition), dry-run
+//     capable (the gpurun box is non-root, settings are read-only).
+// The reference's allocation path could never succeed (both lookup helpers
+// were stubs that always errored, mig_controller.go:340-415); here slice
+// allocation is done by the scheduler ledger and this controller only
+// manages capacity.
+#pragma once
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "discovery.h"
+#include "scheduler.h"
+
+namespace kgwe {
+
+struct PartitionStrategy {
+  std::string name;
+  std::map<std::string, std::string> node_selector;
+  std::string gpu_model;
+  double min_memory_gb = 0.0;
+  std::map<ComputePartition, double> distribution;  // fraction of matching GPUs
+  MemoryPartition memory = MemoryPartition::NPS1;
+  bool allow_dynamic = true;
+  int rebalance_interval_s = 300;
+  double min_utilization = 0.3;  // slices of a mode below this use may shrink
+  int priority = 0;
+};
+
+std::string validate_strategy(const PartitionStrategy& s);  // "" = valid
+PartitionStrategy strategy_from_json(const Json& j);
+Json to_json(const PartitionStrategy& s);
+
+enum class OpState { Pending, Draining, Switching, Completed, Failed };
+const char* to_string(OpState s);
+
+struct PartitionOp {
+  std::string id, node, gpu, reason, error;
+  ComputePartition from = ComputePartition::SPX, to = ComputePartition::SPX;
+  MemoryPartition mem_to = MemoryPartition::NPS1;
+  OpState state = OpState::Pending;
+  bool dry_run = false;
+  int64_t created_ns = 0, finished_ns = 0;
+};
+Json to_json(const PartitionOp& op);
+
+struct PartitionMetrics {
+  struct Mode {
+    int gpus = 0, slices = 0, slices_in_use = 0;
+  };
+  std::map<std::string, Mode> modes;
+  int ops_total = 0, ops_failed = 0, ops_pending = 0;
+  double slice_utilization = 0.0;  // in-use / total over partitioned GPUs
+};
+
+class PartitionController {
+ public:
+  PartitionController(std::shared_ptr<DiscoveryService> disc, std::shared_ptr<Scheduler> sched,
+                      bool dry_run = false);
+
+  std::string register_strategy(const PartitionStrategy& s);  // "" = ok
+  bool remove_strategy(const std::string& name);
+  std::vector<PartitionStrategy> strategies() const;
+
+  // Plan (and unless plan_only, execute) conversions so that `count` free
+  // slices of `mode` exist.  Returns the operations (possibly empty).
+  std::vector<PartitionOp> ensure_capacity(ComputePartition mode, int count, bool plan_only = false);
+  // Move idle GPUs toward a strategy's distribution.
+  std::vector<PartitionOp> rebalance(const std::string& strategy, bool plan_only = false);
+  // Return idle partitioned GPUs with no slice in use back to SPX.
+  std::vector<PartitionOp> reclaim_idle(bool plan_only = false);
+
+  std::vector<PartitionOp> operations() const;
+  PartitionMetrics metrics() const;
+  void set_dry_run(bool d) { dry_run_ = d; }
+
+ private:
+  bool gpu_idle(const GpuDevice& g) const;
+  PartitionOp execute(const std::string& node, const GpuDevice& g, ComputePartition to,
+                      const std::string& reason, bool plan_only);
+  int free_slices(const ClusterTopology& c, ComputePartition mode) const;
+
+  std::shared_ptr<DiscoveryService> disc_;
+  std::shared_ptr<Scheduler> sched_;
+  bool dry_run_;
+  mutable std::mutex mu_;
+  std::map<std::string, PartitionStrategy> strategies_;
+  std::vector<PartitionOp> ops_;
+  int next_op_ = 1;
+};
+
+// ---------------------------------------------------------------------------
+// GPU sharing (reference src/sharing/mig_controller.go:545-857: MPS controller
+// + GPUSharingManager).  ROCm has no MPS daemon; the MI355X-native equivalent
+// of MPS's active-thread percentage is CU masking: each co-located client gets
+// a DISJOINT range of compute units through HSA_CU_MASK, plus a memory cap.
+// ---------------------------------------------------------------------------
+enum class SharingMethod { None, Partition, CoLocate, TimeSlice };
+const char* to_string(SharingMethod m);
+SharingMethod sharing_method_from(const std::string& s);
+
+struct SharingRequest {
+  std::string uid;
+  WorkloadType type = WorkloadType::Inference;
+  bool require_isolation = false;
+  bool prefer_partition = false;
+  ComputePartition partition_mode = ComputePartition::CPX;
+  double cu_percent = 25.0;
+  double memory_gb = 0.0;
+  std::string node, gpu;  // target GPU for co-location / time-slicing
+};
+
+struct SharingAllocation {
+  std::string uid, node, gpu;
+  SharingMethod method = SharingMethod::None;
+  int cu_begin = 0, cu_end = 0;  // [begin, end) for CoLocate
+  double memory_gb = 0.0;
+  int gpu_index = 0;
+  std::map<std::string, std::string> env;  // injected into the pod
+};
+Json to_json(const SharingAllocation& a);
+
+struct SharingPolicy {
+  std::map<WorkloadType, SharingMethod> by_type;
+  int max_clients_per_gpu = 8;
+  double default_cu_percent = 25.0;
+  int max_timeslice_replicas = 4;
+};
+
+class SharingManager {
+ public:
+  SharingManager(std::shared_ptr<DiscoveryService> disc, SharingPolicy policy = {});
+  SharingMethod decide(const SharingRequest& r) const;
+  // Partition method returns method=Partition and leaves slice choice to the
+  // scheduler; CoLocate / TimeSlice allocate here.  error set on failure.
+  SharingAllocation allocate(const SharingRequest& r, std::string* error);
+  bool release(const std::string& uid);
+  std::vector<SharingAllocation> allocations() const;
+  int clients_on(const std::string& gpu) const;
+
+ private:
+  std::shared_ptr<DiscoveryService> disc_;
+  SharingPolicy policy_;
+  mutable std::mutex mu_;
+  std::map<std::string, SharingAllocation> allocs_;
+};
+
+}  // namespace kgwe

@@ -1,0 +1,506 @@
+#include "platform.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+
+namespace kgwe {
+
+namespace {
+
+const Json& field(const Json& j, const char* a, const char* b) {
+  return j.has(a) ? j.get(a) : j.get(b);
+}
+
+double wall_s() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+int64_t quantity(const Json& q) {
+  if (q.is_number()) return q.as_int();
+  return std::atoll(q.str("0").c_str());
+}
+
+}  // namespace
+
+WorkloadRequest workload_from_pod(const Json& pod, const std::string& gpu_resource) {
+  const Json& meta = pod.get("metadata");
+  const Json& ann = meta.get("annotations");
+  const Json& spec = pod.get("spec");
+  WorkloadRequest w;
+  const std::string wl = ann.get("kgwe.amd.com/workload").str();
+  if (!wl.empty()) {
+    try {
+      w = workload_from_json(Json::parse(wl));
+    } catch (...) {
+    }
+  }
+  w.name = meta.get("name").str();
+  w.ns = meta.get("namespace").str("default");
+  w.uid = meta.get("uid").str(w.ns + "/" + w.name);
+  const Json& labels = meta.get("labels");
+  if (w.team.empty()) w.team = labels.get("kgwe.amd.com/team").str(labels.get("team").str());
+  if (w.project.empty()) w.project = labels.get("kgwe.amd.com/project").str();
+  if (wl.empty()) {
+    int64_t gpus = 0;
+    for (const auto& c : spec.get("containers").items()) {
+      const Json& lim = c.get("resources").get("limits");
+      const Json& req = c.get("resources").get("requests");
+      const Json& q = lim.has(gpu_resource) ? lim.get(gpu_resource) : req.get(gpu_resource);
+      gpus += quantity(q);
+      for (const char* mode : {"cpx", "qpx", "dpx"}) {
+        const std::string r = gpu_resource + "-" + mode;
+        const Json& pq = lim.has(r) ? lim.get(r) : req.get(r);
+        const int64_t n = quantity(pq);
+        if (n > 0) {
+          w.partition = true;
+          std::string up = mode;
+          std::transform(up.begin(), up.end(), up.begin(), ::toupper);
+          w.partition_mode = compute_partition_from(up);
+          w.partition_count += static_cast<int>(n);
+        }
+      }
+    }
+    w.gpu_count = static_cast<int>(gpus > 0 ? gpus : (w.partition ? 0 : 1));
+    w.topology = topology_preference_from(ann.get("kgwe.amd.com/topology").str("None"));
+    w.min_memory_gb = std::atof(ann.get("kgwe.amd.com/min-memory-gb").str("0").c_str());
+    w.min_bandwidth_gbps = std::atof(ann.get("kgwe.amd.com/min-bandwidth-gbps").str("0").c_str());
+    w.type = workload_type_from(ann.get("kgwe.amd.com/workload-type").str("Training"));
+    w.strategy = strategy_from(ann.get("kgwe.amd.com/strategy").str("None"));
+    w.gang = ann.get("kgwe.amd.com/gang").str();
+    w.gang_size = std::atoi(ann.get("kgwe.amd.com/gang-size").str("0").c_str());
+    w.preemptible = ann.get("kgwe.amd.com/preemptible").str("true") != "false";
+  }
+  if (spec.has("priority")) w.priority = spec.get("priority").as_int(w.priority);
+  for (const auto& kv : spec.get("nodeSelector").fields()) w.node_selector[kv.first] = kv.second.str();
+  for (const auto& t : spec.get("tolerations").items()) {
+    Toleration tl;
+    tl.key = t.get("key").str();
+    tl.op = t.get("operator").str("Equal");
+    tl.value = t.get("value").str();
+    tl.effect = t.get("effect").str();
+    w.tolerations.push_back(tl);
+  }
+  const Json& na = spec.get("affinity").get("nodeAffinity");
+  for (const auto& term : na.get("requiredDuringSchedulingIgnoredDuringExecution").get("nodeSelectorTerms").items())
+    for (const auto& e : term.get("matchExpressions").items()) {
+      AffinityTerm a;
+      a.key = e.get("key").str();
+      a.op = e.get("operator").str("In");
+      for (const auto& v : e.get("values").items()) a.values.push_back(v.str());
+      w.required_affinity.push_back(a);
+    }
+  for (const auto& pt : na.get("preferredDuringSchedulingIgnoredDuringExecution").items())
+    for (const auto& e : pt.get("preference").get("matchExpressions").items()) {
+      AffinityTerm a;
+      a.key = e.get("key").str();
+      a.op = e.get("operator").str("In");
+      a.weight = static_cast<int>(pt.get("weight").as_int(1));
+      for (const auto& v : e.get("values").items()) a.values.push_back(v.str());
+      w.preferred_affinity.push_back(a);
+    }
+  return w;
+}
+
+std::map<std::string, std::string> rccl_env(const WorkloadRequest& w, const Decision& d,
+                                            const NodeTopology& node, int master_port,
+                                            const std::string& master_addr) {
+  std::map<std::string, std::string> env;
+  // Logical HIP device indices: whole GPUs by index; partition slices are
+  // enumerated GPU-major (every slice is its own HIP device).
+  std::vector<int> idx;
+  std::vector<int> base(node.gpus.size() + 1, 0);
+  std::vector<const GpuDevice*> by_index(node.gpus.size(), nullptr);
+  for (const auto& g : node.gpus)
+    if (g.index >= 0 && g.index < static_cast<int>(by_index.size())) by_index[g.index] = &g;
+  for (size_t i = 0; i < by_index.size(); ++i)
+    base[i + 1] = base[i] + (by_index[i] ? partition_count(by_index[i]->partition.compute) : 1);
+  for (const auto& u : d.gpus)
+    if (const GpuDevice* g = node.gpu(u)) idx.push_back(base[g->index]);
+  for (const auto& p : d.partitions) {
+    auto slash = p.rfind("/p");
+    if (slash == std::string::npos) continue;
+    if (const GpuDevice* g = node.gpu(p.substr(0, slash)))
+      idx.push_back(base[g->index] + std::atoi(p.c_str() + slash + 2));
+  }
+  std::sort(idx.begin(), idx.end());
+  std::string vis;
+  for (size_t i = 0; i < idx.size(); ++i) vis += (i ? "," : "") + std::to_string(idx[i]);
+  const int nproc = static_cast<int>(idx.size());
+  env["HIP_VISIBLE_DEVICES"] = vis;
+  env["ROCR_VISIBLE_DEVICES"] = vis;
+  env["KGWE_ALLOCATED_GPUS"] = [&] {
+    std::string s;
+    for (size_t i = 0; i < d.gpus.size(); ++i) s += (i ? "," : "") + d.gpus[i];
+    for (size_t i = 0; i < d.partitions.size(); ++i) s += (s.empty() ? "" : ",") + d.partitions[i];
+    return s;
+  }();
+  env["KGWE_NODE"] = d.node;
+  char bw[32];
+  std::snprintf(bw, sizeof bw, "%.1f", d.bandwidth_gbps);
+  env["KGWE_XGMI_BANDWIDTH_GBPS"] = bw;
+  if (w.backend == CommBackend::RCCL || w.backend == CommBackend::Gloo) {
+    // torchrun-style rendezvous: one pod = one node's worth of ranks; a
+    // multi-pod gang uses the gang leader's address (set by the controller).
+    const int world = w.world_size > 0 ? w.world_size : std::max(1, nproc);
+    env["NPROC_PER_NODE"] = std::to_string(std::max(1, nproc));
+    env["LOCAL_WORLD_SIZE"] = std::to_string(std::max(1, nproc));
+    env["WORLD_SIZE"] = std::to_string(world);
+    env["NNODES"] = std::to_string(std::max(1, world / std::max(1, nproc)));
+    env["MASTER_ADDR"] = master_addr.empty() ? "127.0.0.1" : master_addr;
+    env["MASTER_PORT"] = std::to_string(master_port);
+    env["TORCH_DISTRIBUTED_BACKEND"] = w.backend == CommBackend::RCCL ? "nccl" : "gloo";
+  }
+  if (w.backend == CommBackend::RCCL) {
+    // RCCL reads the NCCL_* variables.  Single-node xGMI: no IB / sockets on
+    // the data path; dmabuf IPC (legacy IPC mode off) for peer buffers.
+    const bool single_node = w.world_size <= 0 || w.world_size <= nproc;
+    env["NCCL_IB_DISABLE"] = single_node ? "1" : "0";
+    env["NCCL_DEBUG"] = "WARN";
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0";
+    env["NCCL_P2P_LEVEL"] = node.xgmi_fully_connected ? "SYS" : "PHB";
+    env["TORCH_NCCL_ASYNC_ERROR_HANDLING"] = "1";
+    if (nproc == 8 && node.xgmi_fully_connected) env["NCCL_MIN_NCHANNELS"] = "32";  // 7 links x rings
+  }
+  return env;
+}
+
+// ---------------------------------------------------------------------------
+Platform::Platform(PlatformConfig cfg) : cfg_(std::move(cfg)) {
+  disc_ = std::make_shared<DiscoveryService>();
+  sched_ = std::make_shared<Scheduler>(disc_, cfg_.sched);
+  part_ = std::make_shared<PartitionController>(disc_, sched_, cfg_.partition_dry_run);
+  SharingPolicy sp;
+  share_ = std::make_shared<SharingManager>(disc_, sp);
+  cost_ = std::make_shared<CostEngine>(cfg_.cost);
+  reg_ = std::make_shared<MetricRegistry>();
+  reg_->declare_kgwe_families();
+  auto reg = reg_;
+  cost_->set_cost_hook([reg](const UsageRecord& r) {
+    reg->add("kgwe_gpu_cost_total_dollars", {r.ns, r.team}, r.adjusted_cost);
+  });
+}
+
+void Platform::remember_pod(const std::string& uid, const WorkloadRequest& w) {
+  std::lock_guard<std::mutex> lk(pods_mu_);
+  pods_[uid] = w;
+  name_to_uid_[w.ns + "/" + w.name] = uid;
+  if (pods_.size() > 100000) {  // bounded: drop arbitrary old entries
+    pods_.erase(pods_.begin());
+  }
+}
+
+std::string Platform::filter(const std::string& body) {
+  Json out = Json::object();
+  Json args;
+  try {
+    args = Json::parse(body);
+  } catch (const std::exception& e) {
+    out["error"] = std::string("bad ExtenderArgs: ") + e.what();
+    return out.dump();
+  }
+  const Json& pod = field(args, "pod", "Pod");
+  WorkloadRequest w = workload_from_pod(pod, cfg_.gpu_resource);
+  remember_pod(w.uid, w);
+  std::vector<std::string> names;
+  const Json& nodes = field(args, "nodes", "Nodes");
+  const bool full_nodes = nodes.is_object();
+  for (const auto& n : nodes.get("items").items()) names.push_back(n.get("metadata").get("name").str());
+  for (const auto& n : field(args, "nodenames", "NodeNames").items()) names.push_back(n.str());
+  Json failed = Json::object();
+  std::vector<std::string> passed;
+  if (cfg_.enforce_budgets) {
+    // Estimate: one hour of this request at on-demand prices.
+    const GpuPricing p = cost_->pricing("amd-mi355x-288gb");
+    const double est = w.partition ? p.partition.at(to_string(w.partition_mode)) * w.partition_count
+                                   : p.on_demand * w.gpu_count;
+    Admission a = cost_->admit(w.ns, w.team, w.project, est, wall_s());
+    if (!a.allowed) {
+      for (const auto& n : names) failed[n] = a.reason;
+      out["failedNodes"] = failed;
+      out["nodenames"] = Json::array();
+      reg_->add("kgwe_scheduling_failures_total", {"budget"}, 1);
+      return out.dump();
+    }
+  }
+  auto fails = sched_->filter(w, names, &passed);
+  if (passed.empty() && w.partition && cfg_.auto_provision_partitions) {
+    auto ops = part_->ensure_capacity(w.partition_mode, w.partition_count);
+    for (const auto& op : ops)
+      reg_->add("kgwe_partition_reconfigurations_total",
+                {op.node, op.state == OpState::Failed ? "failed" : "ok"}, 1);
+    if (!ops.empty()) {
+      passed.clear();
+      fails = sched_->filter(w, names, &passed);
+    }
+  }
+  for (const auto& kv : fails) failed[kv.first] = kv.second;
+  out["failedNodes"] = failed;
+  if (full_nodes) {
+    Json items = Json::array();
+    for (const auto& n : nodes.get("items").items())
+      if (std::find(passed.begin(), passed.end(), n.get("metadata").get("name").str()) != passed.end())
+        items.push_back(n);
+    Json nl = Json::object();
+    nl["items"] = items;
+    out["nodes"] = nl;
+  } else {
+    Json nn = Json::array();
+    for (const auto& n : passed) nn.push_back(n);
+    out["nodenames"] = nn;
+  }
+  if (passed.empty()) reg_->add("kgwe_scheduling_failures_total", {"filter"}, 1);
+  return out.dump();
+}
+
+std::string Platform::prioritize(const std::string& body) {
+  Json args;
+  try {
+    args = Json::parse(body);
+  } catch (...) {
+    return "[]";
+  }
+  const Json& pod = field(args, "pod", "Pod");
+  WorkloadRequest w = workload_from_pod(pod, cfg_.gpu_resource);
+  std::vector<std::string> names;
+  for (const auto& n : field(args, "nodes", "Nodes").get("items").items())
+    names.push_back(n.get("metadata").get("name").str());
+  for (const auto& n : field(args, "nodenames", "NodeNames").items()) names.push_back(n.str());
+  Json out = Json::array();
+  for (const auto& s : sched_->prioritize(w, names)) {
+    Json h = Json::object();
+    h["host"] = s.node;
+    // kube-scheduler MaxExtenderPriority = 10; our totals are 0..~120.
+    h["score"] = static_cast<int64_t>(std::min(10.0, std::round(s.total / 10.0)));
+    out.push_back(h);
+  }
+  return out.dump();
+}
+
+std::string Platform::placement_json(const WorkloadRequest& w, const Decision& d) {
+  Json pl = to_json(d);
+  NodeTopology n;
+  Json env = Json::object();
+  if (d.ok && disc_->node(d.node, &n)) {
+    for (const auto& kv : rccl_env(w, d, n, cfg_.master_port)) env[kv.first] = kv.second;
+  }
+  pl["env"] = env;
+  pl["workload"] = to_json(w);
+  return pl.dump();
+}
+
+std::string Platform::bind(const std::string& body, const std::string& pod_json) {
+  Json out = Json::object();
+  Json res = Json::object();
+  Json args;
+  try {
+    args = Json::parse(body);
+  } catch (const std::exception& e) {
+    res["error"] = std::string("bad ExtenderBindingArgs: ") + e.what();
+    out["result"] = res;
+    return out.dump();
+  }
+  const std::string name = field(args, "podName", "PodName").str();
+  const std::string ns = field(args, "podNamespace", "PodNamespace").str("default");
+  std::string uid = field(args, "podUID", "PodUID").str();
+  const std::string node = field(args, "node", "Node").str();
+  WorkloadRequest w;
+  bool have = false;
+  if (!pod_json.empty()) {
+    try {
+      w = workload_from_pod(Json::parse(pod_json), cfg_.gpu_resource);
+      have = true;
+    } catch (...) {
+    }
+  }
+  if (!have) {
+    std::lock_guard<std::mutex> lk(pods_mu_);
+    if (uid.empty()) {
+      auto it = name_to_uid_.find(ns + "/" + name);
+      if (it != name_to_uid_.end()) uid = it->second;
+    }
+    auto it = pods_.find(uid);
+    if (it != pods_.end()) {
+      w = it->second;
+      have = true;
+    }
+  }
+  if (!have) {
+    res["error"] = "unknown pod " + ns + "/" + name + " (no filter call seen)";
+    out["result"] = res;
+    return out.dump();
+  }
+  Decision d = sched_->bind(w, node);
+  if (!d.ok) {
+    auto it = d.failed_nodes.find(node);
+    res["error"] = it != d.failed_nodes.end() ? it->second : "bind failed";
+    reg_->add("kgwe_scheduling_failures_total", {"bind"}, 1);
+  } else if (d.status == "Waiting") {
+    // Gang member reserved; kube-scheduler retries bind until the gang is
+    // complete (Permit semantics) or the reservation times out.
+    res["error"] = "gang " + w.gang + " waiting for members";
+  } else {
+    reg_->add("kgwe_scheduling_successes_total", {}, 1);
+    UsageRecord r;
+    r.uid = w.uid;
+    r.ns = w.ns;
+    r.team = w.team;
+    r.project = w.project;
+    r.gpu_type = "amd-mi355x-288gb";
+    r.gpu_count = w.partition ? w.partition_count : w.gpu_count;
+    r.partition_mode = w.partition ? to_string(w.partition_mode) : "";
+    cost_->start(r, wall_s());
+    if (w.partition) reg_->add("kgwe_partition_allocations_total", {to_string(w.partition_mode)}, 1);
+  }
+  reg_->add("kgwe_scheduling_attempts_total", {}, 1);
+  out["result"] = res;
+  out["placement"] = Json::parse(placement_json(w, d));
+  return out.dump();
+}
+
+std::string Platform::schedule(const std::string& workload_json) {
+  WorkloadRequest w = workload_from_json(Json::parse(workload_json));
+  if (w.partition && cfg_.auto_provision_partitions) {
+    Decision probe = sched_->schedule(w);
+    if (probe.ok) return placement_json(w, probe);
+    part_->ensure_capacity(w.partition_mode, w.partition_count);
+  }
+  Decision d = sched_->schedule(w);
+  reg_->add("kgwe_scheduling_attempts_total", {}, 1);
+  if (d.ok) reg_->add("kgwe_scheduling_successes_total", {}, 1);
+  else reg_->add("kgwe_scheduling_failures_total", {"unschedulable"}, 1);
+  reg_->add("kgwe_preemptions_total", {}, static_cast<double>(d.preempted.size()));
+  return placement_json(w, d);
+}
+
+std::string Platform::release(const std::string& uid, double now_s) {
+  Allocation a;
+  const bool had = sched_->allocation(uid, &a);
+  bool ok = sched_->release(uid);
+  share_->release(uid);
+  UsageRecord r;
+  Json out = Json::object();
+  out["released"] = ok;
+  if (cost_->finalize(uid, now_s, &r)) {
+    out["cost"] = to_json(r);
+    reg_->observe("kgwe_workload_duration_seconds", {to_string(a.type)}, r.duration_s);
+  }
+  if (had && !a.partitions.empty()) {
+    GpuDevice g;
+    std::string mode = "CPX";
+    if (disc_->gpu(a.partitions[0].substr(0, a.partitions[0].rfind("/p")), &g))
+      mode = to_string(g.partition.compute);
+    reg_->add("kgwe_partition_releases_total", {mode}, static_cast<double>(a.partitions.size()));
+  }
+  return out.dump();
+}
+
+void Platform::observe_pod_latency_ms(double ms) {
+  reg_->observe("kgwe_scheduling_latency_ms", {}, ms);
+  sched_->record_latency_ms(ms);
+}
+
+void Platform::tick(double now_s) {
+  sched_->expire_gangs();
+  // Feed cost metering with live utilisation of each allocation's GPUs.
+  auto snap = disc_->snapshot();
+  for (const auto& a : sched_->allocations()) {
+    auto it = snap->nodes.find(a.node);
+    if (it == snap->nodes.end()) continue;
+    double gfx = 0, mem = 0;
+    int n = 0;
+    for (const auto& u : a.gpus)
+      if (const GpuDevice* g = it->second.gpu(u)) {
+        gfx += g->util.gfx_activity;
+        mem += g->util.memory_used_pct;
+        ++n;
+      }
+    for (const auto& p : a.partitions)
+      if (const GpuDevice* g = it->second.gpu(p.substr(0, p.rfind("/p")))) {
+        gfx += g->util.gfx_activity;
+        mem += g->util.memory_used_pct;
+        ++n;
+      }
+    if (n) cost_->sample(a.uid, gfx / n, mem / n, now_s);
+  }
+  refresh_gauges(now_s);
+}
+
+void Platform::refresh_gauges(double now_s) {
+  auto snap = disc_->snapshot();
+  for (const char* f : {"kgwe_gpu_count", "kgwe_gpu_utilization_percent", "kgwe_gpu_gfx_activity_percent",
+                        "kgwe_gpu_umc_activity_percent", "kgwe_gpu_memory_used_bytes",
+                        "kgwe_gpu_memory_total_bytes", "kgwe_gpu_temperature_celsius", "kgwe_gpu_power_watts",
+                        "kgwe_gpu_health_status", "kgwe_gpu_hbm_bandwidth_gbps", "kgwe_gpu_ecc_errors_total",
+                        "kgwe_gpu_partition_mode", "kgwe_partition_instance_count",
+                        "kgwe_partition_instance_utilization_percent", "kgwe_xgmi_bandwidth_gbps",
+                        "kgwe_xgmi_link_status", "kgwe_pcie_bandwidth_gbps", "kgwe_topology_score",
+                        "kgwe_active_workloads", "kgwe_budget_utilization_percent",
+                        "kgwe_cost_savings_recommended_dollars", "kgwe_gpu_cost_per_hour_dollars"})
+    reg_->clear(f);
+  std::set<std::string> owned_parts;
+  for (const auto& a : sched_->allocations())
+    for (const auto& p : a.partitions) owned_parts.insert(p);
+  for (const auto& kv : snap->nodes) {
+    const NodeTopology& n = kv.second;
+    reg_->set("kgwe_gpu_count", {n.name}, static_cast<double>(n.gpus.size()));
+    std::map<std::string, std::pair<int, int>> slices;  // mode -> (used, total)
+    int links_up = 0, links = 0;
+    for (const auto& g : n.gpus) {
+      reg_->set("kgwe_gpu_utilization_percent", {g.uuid, n.name, g.model}, g.util.gfx_activity);
+      reg_->set("kgwe_gpu_gfx_activity_percent", {g.uuid, n.name}, g.util.gfx_activity);
+      reg_->set("kgwe_gpu_umc_activity_percent", {g.uuid, n.name}, g.util.umc_activity);
+      reg_->set("kgwe_gpu_memory_used_bytes", {g.uuid, n.name}, g.memory_used_gb * 1073741824.0);
+      reg_->set("kgwe_gpu_memory_total_bytes", {g.uuid, n.name}, g.memory_total_gb * 1073741824.0);
+      reg_->set("kgwe_gpu_temperature_celsius", {g.uuid, n.name}, g.util.temperature_c);
+      reg_->set("kgwe_gpu_power_watts", {g.uuid, n.name}, g.util.power_w);
+      reg_->set("kgwe_gpu_health_status", {g.uuid, n.name},
+                g.health.status == HealthStatus::Healthy ? 1.0
+                : g.health.status == HealthStatus::Degraded ? 0.5 : 0.0);
+      if (g.hbm_measured_gbps > 0) reg_->set("kgwe_gpu_hbm_bandwidth_gbps", {g.uuid, n.name}, g.hbm_measured_gbps);
+      reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "correctable"}, static_cast<double>(g.health.ecc_correctable));
+      reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "uncorrectable"}, static_cast<double>(g.health.ecc_uncorrectable));
+      reg_->set("kgwe_gpu_partition_mode", {g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0);
+      reg_->set("kgwe_partition_instance_count", {g.uuid, n.name, to_string(g.partition.compute)},
+                static_cast<double>(g.partition.instances.size()));
+      auto& sl = slices[to_string(g.partition.compute)];
+      for (const auto& pi : g.partition.instances) {
+        sl.second++;
+        sl.first += (pi.in_use || owned_parts.count(pi.id)) ? 1 : 0;
+      }
+      reg_->set("kgwe_pcie_bandwidth_gbps", {g.uuid, n.name}, g.pcie.bandwidth_gbps);
+      for (const auto& l : g.links) {
+        reg_->set("kgwe_xgmi_bandwidth_gbps", {g.uuid, l.peer_uuid, n.name}, l.up ? l.effective_gbps() : 0.0);
+        reg_->set("kgwe_xgmi_link_status", {g.uuid, l.peer_uuid, n.name}, l.up ? 1.0 : 0.0);
+        ++links;
+        links_up += l.up && l.type == LinkType::XGMI;
+      }
+    }
+    for (const auto& s : slices)
+      if (s.first != "SPX")
+        reg_->set("kgwe_partition_instance_utilization_percent", {n.name, s.first},
+                  s.second.second ? 100.0 * s.second.first / s.second.second : 0.0);
+    // Node topology score: 50 base, +30 full xGMI mesh, +20 proportional link health.
+    double ts = 50.0 + (n.xgmi_fully_connected ? 30.0 : 0.0) + (links ? 20.0 * links_up / links : 0.0);
+    reg_->set("kgwe_topology_score", {n.name}, ts);
+  }
+  std::map<std::pair<std::string, std::string>, int> active;
+  for (const auto& a : sched_->allocations()) active[{a.ns, to_string(a.type)}]++;
+  for (const auto& kv : active)
+    reg_->set("kgwe_active_workloads", {kv.first.first, kv.first.second}, kv.second);
+  for (const auto& b : cost_->budgets(now_s))
+    reg_->set("kgwe_budget_utilization_percent", {b.id, to_string(b.scope)},
+              b.limit > 0 ? 100.0 * b.spend / b.limit : 0.0);
+  std::map<std::string, double> saving;
+  for (const auto& r : cost_->recommendations("", "")) saving[r.type] += r.saving;
+  for (const auto& kv : saving) reg_->set("kgwe_cost_savings_recommended_dollars", {kv.first}, kv.second);
+  reg_->set("kgwe_gpu_cost_per_hour_dollars", {"all"}, cost_->running_cost_per_hour());
+  reg_->set("kgwe_workload_queue_depth", {}, 0.0);
+}
+
+std::string Platform::expose_metrics() {
+  refresh_gauges(wall_s());
+  return reg_->expose();
+}
+
+}  // namespace kgwe

@@ -1,0 +1,98 @@
+// The kgwe control plane wired end to end, with the kube-scheduler EXTENDER
+// wire contract handled natively (JSON in -> JSON out).
+//
+// Reference: the extender contract exists only as configuration
+// (deploy/helm/kgwe/templates/scheduler-configmap.yaml:61-79: verbs filter /
+// prioritize / bind, weight 100, nodeCacheCapable false, managed resources);
+// no server, no glue and no constructor calls exist.  Here:
+//   filter      ExtenderArgs          -> ExtenderFilterResult
+//                 (+ budget admission, + partition auto-provisioning — the
+//                  designed PreBind "KGWEMIGProvisioning" plugin)
+//   prioritize  ExtenderArgs          -> HostPriorityList (0..10)
+//   bind        ExtenderBindingArgs   -> ExtenderBindingResult + the placement
+//                 (GPUs / slices, RCCL-over-xGMI rank env, CU masks) that the
+//                 Python shell writes to the apiserver (Binding + annotations);
+//                 starts cost metering (the designed PostBind
+//                 "KGWECostTracking" plugin) and records metrics.
+// The HTTP socket handling lives in the Python shell (kgwe/extender); every
+// byte of request parsing, scoring and response building is here.
+#pragma once
+#include <memory>
+#include <string>
+
+#include "cost.h"
+#include "discovery.h"
+#include "metrics.h"
+#include "partition.h"
+#include "scheduler.h"
+
+namespace kgwe {
+
+struct PlatformConfig {
+  SchedulerConfig sched;
+  CostEngineConfig cost;
+  bool partition_dry_run = false;
+  bool auto_provision_partitions = true;
+  bool enforce_budgets = true;
+  int master_port = 29500;
+  std::string gpu_resource = "amd.com/gpu";
+};
+
+// Pod (core/v1 JSON) -> workload request.  Sources, in order: annotation
+// kgwe.amd.com/workload (a GPUWorkload spec), amd.com/gpu limits,
+// amd.com/gpu-<mode> partition resources, kgwe.amd.com/* annotations,
+// spec.priority / nodeSelector / tolerations / nodeAffinity.
+WorkloadRequest workload_from_pod(const Json& pod, const std::string& gpu_resource = "amd.com/gpu");
+
+// RCCL-over-xGMI rank environment for a placement.
+std::map<std::string, std::string> rccl_env(const WorkloadRequest& w, const Decision& d,
+                                            const NodeTopology& node, int master_port,
+                                            const std::string& master_addr = "");
+
+class Platform {
+ public:
+  explicit Platform(PlatformConfig cfg = {});
+
+  std::shared_ptr<DiscoveryService> discovery() { return disc_; }
+  std::shared_ptr<Scheduler> scheduler() { return sched_; }
+  std::shared_ptr<PartitionController> partitions() { return part_; }
+  std::shared_ptr<SharingManager> sharing() { return share_; }
+  std::shared_ptr<CostEngine> cost() { return cost_; }
+  std::shared_ptr<MetricRegistry> metrics() { return reg_; }
+
+  // Extender verbs (bodies are JSON text).
+  std::string filter(const std::string& body);
+  std::string prioritize(const std::string& body);
+  // Returns {"result": ExtenderBindingResult, "placement": {...}}.
+  std::string bind(const std::string& body, const std::string& pod_json = "");
+
+  // Direct API (controller / optimizer / tests).
+  std::string schedule(const std::string& workload_json);
+  std::string release(const std::string& uid, double now_s);
+  void observe_pod_latency_ms(double ms);
+
+  // Periodic sweep: gang timeouts, cost samples from telemetry, gauges.
+  void tick(double now_s);
+  std::string expose_metrics();
+
+  // Remember the pod object for a uid between filter and bind (the bind
+  // request only carries name/namespace/uid/node).
+  void remember_pod(const std::string& uid, const WorkloadRequest& w);
+
+ private:
+  std::string placement_json(const WorkloadRequest& w, const Decision& d);
+  void refresh_gauges(double now_s);
+
+  PlatformConfig cfg_;
+  std::shared_ptr<DiscoveryService> disc_;
+  std::shared_ptr<Scheduler> sched_;
+  std::shared_ptr<PartitionController> part_;
+  std::shared_ptr<SharingManager> share_;
+  std::shared_ptr<CostEngine> cost_;
+  std::shared_ptr<MetricRegistry> reg_;
+  std::mutex pods_mu_;
+  std::map<std::string, WorkloadRequest> pods_;  // uid -> request (filter -> bind)
+  std::map<std::string, std::string> name_to_uid_;
+};
+
+}  // namespace kgwe

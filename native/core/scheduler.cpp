@@ -1281,6 +1281,14 @@ bool Scheduler::restore(const Allocation& a) {
   return true;
 }
 
+bool Scheduler::gpu_busy(const GpuDevice& g) const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  if (gpu_owner_.count(g.uuid)) return true;
+  for (const auto& pi : g.partition.instances)
+    if (part_owner_.count(pi.id)) return true;
+  return false;
+}
+
 std::vector<Allocation> Scheduler::allocations() const {
   std::shared_lock<std::shared_mutex> lk(mu_);
   std::vector<Allocation> out;

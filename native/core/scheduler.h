@@ -192,6 +192,8 @@ class Scheduler {
   // Restore the ledger (controller restart: rebuilt from pod annotations).
   bool restore(const Allocation& a);
 
+  // True when the GPU or any of its partition slices is held in the ledger.
+  bool gpu_busy(const GpuDevice& g) const;
   std::vector<Allocation> allocations() const;
   bool allocation(const std::string& uid, Allocation* out) const;
   SchedulerMetrics metrics() const;
