@@ -52,11 +52,20 @@ def parse(argv=None):
 
 
 def run_scheduling_bench(args, world: int) -> dict | None:
+    """Runs in its own child process tree (apiserver / scheduler / extender),
+    started before this process touches the GPU."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "kgwe.bench.sched_latency", "--json", "--pods",
+           str(args.sched_pods), "--job-gpus", str(world)]
     try:
-        from kgwe.bench.sched_latency import run as sched_run
-    except ImportError:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=400,
+                           cwd=os.path.dirname(os.path.abspath(__file__)))
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        return json.loads(line)
+    except Exception as e:  # noqa: BLE001 - report, never fake a number
+        print(f"[bench] scheduling benchmark failed: {e}", file=sys.stderr)
         return None
-    return sched_run(n_pods=args.sched_pods, job_gpus=world)
 
 
 def main(argv=None) -> int:
@@ -69,14 +78,14 @@ def main(argv=None) -> int:
 
     if args.sdpa:
         attn_ops.set_force_sdpa(True)
+    # Scheduling benchmark first (rank 0, CPU only, before any GPU init).
+    sched = None
+    if int(os.environ.get("RANK", "0")) == 0 and not args.no_sched:
+        sched = run_scheduling_bench(args, int(os.environ.get("WORLD_SIZE", "1")))
     info = kdist.init(force_group=True)
     world = info.world_size
     if args.gpus != world and info.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-
-    sched = None
-    if info.is_main and not args.no_sched:
-        sched = run_scheduling_bench(args, world)
 
     tc = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
                      activation_checkpointing=args.ckpt)

@@ -1,0 +1,157 @@
+"""kube-scheduler extender HTTP server (filter / prioritize / bind).
+
+Implements the contract declared by the reference's scheduler ConfigMap
+(deploy/helm/kgwe/templates/scheduler-configmap.yaml:61-79: urlPrefix on the
+controller service :8080, verbs filter / prioritize / bind, weight 100,
+nodeCacheCapable false, ignorable false) — which the reference never served
+(SURVEY.md D1/N7).  This module is only socket plumbing: request bodies go
+straight into the C++ core (``kgwe.core.Platform``) and its JSON replies go
+straight back; the GIL is released inside the core so concurrent extender
+calls score in parallel.
+
+On a successful bind the shell also:
+  * POSTs the pods/binding subresource to the apiserver;
+  * writes the placement to pod annotations (kgwe.amd.com/allocated-gpus,
+    kgwe.amd.com/rccl-env, ...) — consumed at container start by
+    ``kgwe.launch`` (downward API) to export HIP_VISIBLE_DEVICES and the RCCL
+    rank environment;
+  * records the pod-create -> bind latency into the p99 histogram.
+"""
+from __future__ import annotations
+
+import json
+import threading
+import time
+from datetime import datetime, timezone
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from ..core import Platform
+from ..utils import tracing
+
+ANN_GPUS = "kgwe.amd.com/allocated-gpus"
+ANN_PARTS = "kgwe.amd.com/allocated-partitions"
+ANN_ENV = "kgwe.amd.com/rccl-env"
+ANN_NODE = "kgwe.amd.com/node"
+ANN_SCORE = "kgwe.amd.com/score"
+ANN_BW = "kgwe.amd.com/estimated-bandwidth-gbps"
+
+
+def _created_s(meta: dict) -> float | None:
+    ts = meta.get("creationTimestamp")
+    if not ts:
+        return None
+    try:
+        return datetime.strptime(ts, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=timezone.utc).timestamp()
+    except ValueError:
+        return None
+
+
+class ExtenderServer:
+    def __init__(self, platform: Platform, kube=None, host: str = "0.0.0.0", port: int = 8080,
+                 url_prefix: str = ""):
+        self.platform = platform
+        self.kube = kube
+        self.prefix = url_prefix.rstrip("/")
+        self.tracer = tracing.PhaseTimer()
+        outer = self
+
+        class H(BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+            disable_nagle_algorithm = True
+
+            def log_message(self, *a):
+                pass
+
+            def _send(self, code: int, data: bytes, ctype="application/json"):
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+            def do_GET(self):
+                p = self.path.split("?")[0]
+                if p in ("/healthz", "/health", "/readyz"):
+                    return self._send(200, b"ok", "text/plain")
+                if p == "/metrics":
+                    return self._send(200, outer.platform.expose_metrics().encode(),
+                                      "text/plain; version=0.0.4")
+                if p == "/debug/allocations":
+                    return self._send(200, json.dumps(outer.platform.allocations()).encode())
+                if p == "/debug/scheduler":
+                    m = outer.platform.scheduler_metrics()
+                    m["phases"] = outer.tracer.summary()
+                    return self._send(200, json.dumps(m).encode())
+                if p == "/debug/topology":
+                    return self._send(200, json.dumps(outer.platform.snapshot()).encode())
+                return self._send(404, b'{"error":"not found"}')
+
+            def do_POST(self):
+                n = int(self.headers.get("Content-Length") or 0)
+                body = self.rfile.read(n).decode() if n else "{}"
+                verb = self.path.split("?")[0][len(outer.prefix):].strip("/")
+                try:
+                    if verb == "filter":
+                        with outer.tracer.phase("filter"):
+                            out = outer.platform.filter(body)
+                    elif verb == "prioritize":
+                        with outer.tracer.phase("prioritize"):
+                            out = outer.platform.prioritize(body)
+                    elif verb == "bind":
+                        with outer.tracer.phase("bind"):
+                            out = json.dumps(outer.handle_bind(body))
+                    else:
+                        return self._send(404, b'{"error":"unknown verb"}')
+                except Exception as e:  # noqa: BLE001 - contract: errors go in the body
+                    out = json.dumps({"error": f"{type(e).__name__}: {e}"})
+                return self._send(200, out.encode())
+
+        self.httpd = ThreadingHTTPServer((host, port), H)
+        self.httpd.daemon_threads = True
+        self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
+
+    @property
+    def url(self) -> str:
+        h, p = self.httpd.server_address[:2]
+        return f"http://{h}:{p}{self.prefix}"
+
+    def handle_bind(self, body: str) -> dict:
+        args = json.loads(body)
+        ns = args.get("podNamespace") or args.get("PodNamespace") or "default"
+        name = args.get("podName") or args.get("PodName")
+        uid = args.get("podUID") or args.get("PodUID") or ""
+        node = args.get("node") or args.get("Node")
+        pod = None
+        res = self.platform.bind(body)
+        result = res.get("result", {})
+        if result.get("error") and "no filter call seen" in result["error"] and self.kube is not None:
+            pod = self.kube.get_pod(ns, name)  # extender restarted between verbs
+            res = self.platform.bind(body, pod)
+            result = res.get("result", {})
+        if result.get("error"):
+            return result
+        pl = res["placement"]
+        if self.kube is not None:
+            ann = {ANN_GPUS: ",".join(pl.get("gpus", [])), ANN_PARTS: ",".join(pl.get("partitions", [])),
+                   ANN_ENV: json.dumps(pl.get("env", {}), sort_keys=True), ANN_NODE: node,
+                   ANN_SCORE: str(pl.get("score", 0)), ANN_BW: f"{pl.get('bandwidth_gbps', 0.0):.1f}"}
+            try:
+                self.kube.patch_pod(ns, name, {"metadata": {"annotations": ann}})
+                self.kube.bind_pod(ns, name, node, uid)
+            except Exception as e:  # noqa: BLE001
+                self.platform.release(pl.get("uid") or uid)
+                return {"error": f"binding failed: {e}"}
+            if pod is None:
+                pod = {"metadata": {}}
+            created = _created_s(pod.get("metadata", {}))
+            if created is not None:
+                self.platform.observe_pod_latency_ms(max(0.0, (time.time() - created) * 1000.0))
+        return {}
+
+    def start(self) -> "ExtenderServer":
+        self.thread.start()
+        return self
+
+    def stop(self) -> None:
+        self.httpd.shutdown()
+        self.httpd.server_close()
