@@ -1,0 +1,226 @@
+"""Scheduler core (C++) — placement, filters, preemption, gangs, ledger safety.
+
+Maps to SURVEY.md §4 test plan items 1/3: scorers against the reference
+formulas (compat mode), every filter constraint, ledger atomicity under
+concurrency, bounded priority-aware preemption, gang all-or-nothing, and a p99
+that comes from the histogram (not a running max).
+"""
+import json
+import threading
+
+import pytest
+
+from kgwe.core import Platform, make_fixture
+
+
+def wl(uid, count=1, topo="None", **spec):
+    s = {"gpuRequirements": {"count": count, "topology": {"preference": topo}}}
+    s["gpuRequirements"].update(spec.pop("req", {}))
+    s.update(spec)
+    return {"metadata": {"name": uid, "namespace": "ns", "uid": uid}, "spec": s}
+
+
+@pytest.fixture
+def plat():
+    p = Platform({})
+    for i in range(2):
+        p.add_fake_node(make_fixture(f"n{i}", 8, 2))
+    return p
+
+
+def test_single_gpu_best_fit(plat):
+    d = plat.schedule(wl("a", 1))
+    assert d["ok"] and len(d["gpus"]) == 1 and d["score"] > 0
+    # second single-GPU job packs into the same NUMA domain (best fit)
+    d2 = plat.schedule(wl("b", 1))
+    snap = plat.snapshot()
+    numa = {g["uuid"]: g["numa_node"] for n in snap["nodes"].values() for g in n["gpus"]}
+    if d2["node"] == d["node"]:
+        assert numa[d2["gpus"][0]] == numa[d["gpus"][0]]
+
+
+def test_xgmi_group_prefers_single_numa_domain(plat):
+    d = plat.schedule(wl("j4", 4, "xGMIOptimal"))
+    assert d["ok"]
+    snap = plat.snapshot()
+    numa = {g["uuid"]: g["numa_node"] for n in snap["nodes"].values() for g in n["gpus"]}
+    assert len({numa[g] for g in d["gpus"]}) == 1
+    assert d["score"] >= 80
+
+
+def test_eight_gpu_fsdp_job_gets_whole_node_and_rccl_env(plat):
+    d = plat.schedule(wl("fsdp", 8, "xGMIOptimal",
+                         distributedConfig={"strategy": "FSDP", "worldSize": 8, "backend": "RCCL"}))
+    assert d["ok"] and len(d["gpus"]) == 8
+    env = d["env"]
+    assert env["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7"
+    assert env["WORLD_SIZE"] == "8" and env["NPROC_PER_NODE"] == "8"
+    assert env["TORCH_DISTRIBUTED_BACKEND"] == "nccl"  # RCCL on ROCm
+    assert env["NCCL_IB_DISABLE"] == "1" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert float(env["KGWE_XGMI_BANDWIDTH_GBPS"]) > 100
+
+
+def test_down_link_breaks_clique_for_xgmi_required(plat):
+    uu = [f"GPU-n0-{i:02d}" for i in range(8)]
+    for j in range(1, 8):
+        plat.fake_set_link_up("n0", uu[0], uu[j], False)
+    # n1 busy so only n0 is a candidate
+    assert plat.schedule(wl("fill", 8, "None", constraints={"nodeSelector": {"kubernetes.io/hostname": "n1"}}))["ok"]
+    d = plat.schedule(wl("req8", 8, "xGMIRequired"))
+    assert not d["ok"]
+    assert "xGMI" in d["failed_nodes"]["n0"]
+    d7 = plat.schedule(wl("req7", 7, "xGMIRequired"))
+    assert d7["ok"] and uu[0] not in d7["gpus"]
+
+
+def test_degraded_measured_link_avoided(plat):
+    a, b = "GPU-n0-00", "GPU-n0-01"
+    plat.fake_set_measured_link("n0", a, b, 20.0)
+    plat.fake_set_measured_link("n0", b, a, 20.0)
+    plat.schedule(wl("x", 8, "None", constraints={"nodeSelector": {"kubernetes.io/hostname": "n1"}}))
+    d = plat.schedule(wl("pair", 2, "xGMIOptimal"))
+    assert d["ok"] and not ({a, b} <= set(d["gpus"]))
+
+
+@pytest.mark.parametrize("field,value,expect", [
+    ("nodeSelector", {"kubernetes.io/hostname": "n1"}, "n1"),
+    ("excludeNodes", ["n0"], "n1"),
+])
+def test_constraints(plat, field, value, expect):
+    d = plat.schedule(wl("c", 1, constraints={field: value}))
+    assert d["ok"] and d["node"] == expect
+
+
+def test_taints_and_tolerations():
+    p = Platform({})
+    fx = make_fixture("t0", 8, 2)
+    fx["taints"] = [{"key": "dedicated", "value": "llm", "effect": "NoSchedule"}]
+    p.add_fake_node(fx)
+    assert not p.schedule(wl("no", 1))["ok"]
+    ok = p.schedule(wl("yes", 1, constraints={"tolerations": [
+        {"key": "dedicated", "operator": "Equal", "value": "llm", "effect": "NoSchedule"}]}))
+    assert ok["ok"]
+
+
+def test_min_memory_and_unhealthy(plat):
+    plat.fake_set_health("n0", "GPU-n0-03", "Unhealthy", "uncorrectable ECC")
+    plat.schedule(wl("big", 8, constraints={"nodeSelector": {"kubernetes.io/hostname": "n1"}}))
+    d = plat.schedule(wl("seven", 8))
+    assert not d["ok"]  # n0 has only 7 healthy GPUs
+    assert not plat.schedule(wl("huge", 1, req={"minMemoryGB": 300}))["ok"]
+
+
+def test_anti_affinity_and_colocation(plat):
+    a = plat.schedule(wl("a", 1))
+    b = plat.schedule(wl("b", 1, constraints={"antiAffinityWith": ["a"]}))
+    assert b["ok"] and b["node"] != a["node"]
+    c = plat.schedule(wl("c", 1, constraints={"colocateWith": ["a"]}))
+    assert c["ok"] and c["node"] == a["node"]
+
+
+def test_preemption_respects_priority_and_preemptible(plat):
+    for i, n in enumerate(["n0", "n1"]):
+        assert plat.schedule(wl(f"low{i}", 8, priority=10,
+                                constraints={"nodeSelector": {"kubernetes.io/hostname": n}}))["ok"]
+    # equal priority: no preemption
+    assert not plat.schedule(wl("eq", 8, priority=10))["ok"]
+    d = plat.schedule(wl("high", 8, priority=100))
+    assert d["ok"] and len(d["preempted"]) == 1
+    # non-preemptible victims are never chosen
+    p = Platform({})
+    p.add_fake_node(make_fixture("m0", 8, 2))
+    assert p.schedule(wl("np", 8, priority=1, preemptible=False))["ok"]
+    assert not p.schedule(wl("hi", 8, priority=1000))["ok"]
+
+
+def test_gang_all_or_nothing(plat):
+    members = [wl(f"g{i}", 8, "xGMIOptimal") for i in range(3)]
+    res = plat.schedule_gang(members)
+    assert not any(r["ok"] for r in res)  # 3 x 8 GPUs > 16 GPUs
+    assert plat.scheduler_metrics()["allocated_gpus"] == 0
+    res = plat.schedule_gang(members[:2])
+    assert all(r["ok"] for r in res) and {r["node"] for r in res} == {"n0", "n1"}
+
+
+def test_gang_member_waits_until_complete(plat):
+    g = {"name": "ring", "size": 2}
+    d1 = plat.schedule(wl("m1", 2, gang=g))
+    assert d1["ok"] and d1["status"] == "Waiting"
+    assert plat.permit("m1") == "Wait"
+    d2 = plat.schedule(wl("m2", 2, gang=g))
+    assert d2["status"] == "Scheduled"
+    assert plat.permit("m1") == "Allow" and plat.permit("m2") == "Allow"
+
+
+def test_gang_timeout_releases_reservations():
+    p = Platform({"scheduler": {"gangTimeoutMs": 1}})
+    p.add_fake_node(make_fixture("z", 8, 2))
+    assert p.schedule(wl("only", 4, gang={"name": "gg", "size": 2}))["status"] == "Waiting"
+    import time
+    time.sleep(0.01)
+    assert p.permit("only") == "Reject"
+    assert p.scheduler_metrics()["allocated_gpus"] == 0
+
+
+def test_concurrent_schedule_never_double_allocates():
+    p = Platform({"scheduler": {"enablePreemption": False}})
+    for i in range(4):
+        p.add_fake_node(make_fixture(f"c{i}", 8, 2))
+    results = []
+    lock = threading.Lock()
+
+    def worker(k):
+        for j in range(20):
+            d = p.schedule(wl(f"w{k}-{j}", 1 + (j % 3)))
+            with lock:
+                results.append(d)
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    owned = [g for d in results if d["ok"] for g in d["gpus"]]
+    assert len(owned) == len(set(owned)), "a GPU was allocated twice"
+    assert len(owned) <= 32
+    assert p.scheduler_metrics()["allocated_gpus"] == len(owned)
+
+
+def test_release_and_events(plat):
+    d = plat.schedule(wl("r", 2))
+    assert plat.release("r")["released"]
+    assert not plat.release("r")["released"]
+    evs = [e["type"] for e in plat.scheduler_events()]
+    assert "Scheduled" in evs and "Released" in evs
+
+
+def test_p99_is_a_quantile_not_max():
+    p = Platform({})
+    for _ in range(1000):
+        p.observe_pod_latency_ms(1.0)
+    p.observe_pod_latency_ms(5000.0)
+    m = p.scheduler_metrics()
+    assert m["p99_ms"] < 2.0 and m["max_ms"] >= 5000.0
+
+
+def test_compat_mode_reproduces_reference_formulas():
+    p = Platform({"scheduler": {"scoring": "compat"}})
+    p.add_fake_node(make_fixture("k", 8, 2))
+    s = p.score_node("k", wl("q", 2, "xGMIOptimal"))
+    # reference: 50 + 50 * bw / (900 * C(k,2)) with 153.6 GB/s xGMI links
+    assert s["topology"] == int(50 + 50 * 153.6 / 900)
+    s = p.score_node("k", wl("q", 1))
+    assert s["topology"] == 100
+    assert s["resource"] == 100 and s["balance"] == 100
+    assert s["total"] == (100 * 40 + 100 * 35 + 100 * 25) // 100
+
+
+def test_optimizer_hint_bonus(plat):
+    s0 = plat.score_node("n1", wl("h", 1))
+    s1 = plat.score_node("n1", wl("h", 1, preferredNodes=["n1"]))
+    assert s1["total"] == s0["total"] + 10
+
+
+def test_topology_hints(plat):
+    hs = plat.hints(4)
+    assert hs and hs[0]["score"] >= 80 and len(hs[0]["gpus"]) == 4
+    assert "fully connected xGMI group" in hs[0]["reasons"]
