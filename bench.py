@@ -70,6 +70,9 @@ def run_scheduling_bench(args, world: int) -> dict | None:
 
 def main(argv=None) -> int:
     args = parse(argv)
+    import faulthandler
+
+    faulthandler.dump_traceback_later(900, exit=False)  # stack dump if a phase hangs
     import torch
 
     from kgwe.bench.train import TrainConfig, Trainer, timed_run

@@ -74,6 +74,25 @@ PRESETS = {
 }
 
 
+class RopeCache:
+    """fp32 cos/sin tables [S, head_dim/2] per (S, device); a plain object (not
+    an nn.Module / buffer) so FSDP neither shards nor casts it."""
+
+    _tables: dict = {}
+
+    def __init__(self, cfg: "LlamaConfig"):
+        self.head_dim = cfg.head_dim
+        self.theta = cfg.rope_theta
+
+    def __call__(self, seq_len: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+        key = (seq_len, self.head_dim, self.theta, str(device))
+        t = RopeCache._tables.get(key)
+        if t is None:
+            t = ref.rope_tables(seq_len, self.head_dim, self.theta, device)
+            RopeCache._tables[key] = t
+        return t
+
+
 class Attention(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
@@ -111,11 +130,15 @@ class TransformerBlock(nn.Module):
         self.feed_forward = FeedForward(cfg)
         self.attention_norm = nn.Parameter(torch.ones(cfg.dim))
         self.ffn_norm = nn.Parameter(torch.ones(cfg.dim))
+        self.rope_tables = RopeCache(cfg)
 
-    def forward(self, x, residual, cos, sin):
+    def forward(self, x, residual):
         """(x, residual) -> (mlp_out, residual'); the residual add happens inside
-        the next RMSNorm kernel."""
+        the next RMSNorm kernel.  RoPE tables come from the shared cache, NOT
+        from forward args: FSDP2's MixedPrecisionPolicy casts floating-point
+        forward inputs to bf16, which would corrupt the fp32 cos/sin tables."""
         eps = self.cfg.norm_eps
+        cos, sin = self.rope_tables(x.shape[1], x.device)
         if residual is None:
             xn, residual = K.rmsnorm(x, self.attention_norm, eps)
         else:
@@ -133,7 +156,6 @@ class Llama(nn.Module):
         self.layers = nn.ModuleList(TransformerBlock(cfg) for _ in range(cfg.n_layers))
         self.norm = nn.Parameter(torch.ones(cfg.dim))
         self.output = nn.Parameter(torch.empty(cfg.vocab_size, cfg.dim))
-        self._rope_cache: dict = {}
         self.activation_checkpointing = False
 
     @torch.no_grad()
@@ -145,24 +167,15 @@ class Llama(nn.Module):
             else:
                 p.normal_(0.0, std, generator=g)
 
-    def rope(self, seq_len: int, device) -> tuple[torch.Tensor, torch.Tensor]:
-        key = (seq_len, str(device))
-        if key not in self._rope_cache:
-            self._rope_cache[key] = ref.rope_tables(seq_len, self.cfg.head_dim,
-                                                    self.cfg.rope_theta, device)
-        return self._rope_cache[key]
-
     def forward_hidden(self, tokens: torch.Tensor) -> torch.Tensor:
-        B, S = tokens.shape
-        cos, sin = self.rope(S, tokens.device)
         h = self.tok_embeddings(tokens)
         residual = None
         for layer in self.layers:
             if self.activation_checkpointing and torch.is_grad_enabled():
                 h, residual = torch.utils.checkpoint.checkpoint(
-                    layer, h, residual, cos, sin, use_reentrant=False)
+                    layer, h, residual, use_reentrant=False)
             else:
-                h, residual = layer(h, residual, cos, sin)
+                h, residual = layer(h, residual)
         h, _ = K.rmsnorm(h, self.norm, self.cfg.norm_eps, residual=residual)
         return h
 

@@ -57,7 +57,12 @@ class FusedAdamW(torch.optim.Optimizer):
         tens = np.zeros(len(ps), dtype=_TENSOR_DT)
         chunks = []
         for i, (p, g, m, v) in enumerate(zip(ps, gs, ms, vs)):
-            assert p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous()
+            # Kernel contract: fp32, contiguous, equal element counts.
+            if not (p.dtype == g.dtype == m.dtype == v.dtype == torch.float32
+                    and p.is_contiguous() and g.is_contiguous()
+                    and p.numel() == g.numel() == m.numel() == v.numel()):
+                raise ValueError(f"FusedAdamW: tensor {i} violates the kernel contract "
+                                 f"(p {p.dtype}/{p.shape}, g {g.dtype}/{g.shape})")
             tens[i] = (p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), 0, p.numel())
             for s in range(0, p.numel(), chunk):
                 chunks.append((i, 0, s))

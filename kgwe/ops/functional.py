@@ -12,6 +12,13 @@ from . import reference as ref
 from ._lib import check, lib, ptr, stream, use_hip
 
 
+def _require(cond: bool, msg: str) -> None:
+    """Shape/dtype contract of a HIP kernel, checked on the host before launch
+    (an out-of-contract launch would read or write out of bounds)."""
+    if not cond:
+        raise ValueError(msg)
+
+
 # --------------------------------------------------------------------------
 # RMSNorm (+ fused residual add)
 # --------------------------------------------------------------------------
@@ -59,7 +66,13 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5,
             residual: torch.Tensor | None = None):
     """Returns (normed, h) where h = x + residual (the new residual stream)."""
     if use_hip(x):
-        assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+        H = x.shape[-1]
+        _require(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16,
+                 "rmsnorm: x and w must be bf16")
+        _require(H in (512, 1024, 2048, 4096, 8192) and w.numel() == H,
+                 "rmsnorm: hidden size must be 512*2^k <= 8192 and w [H]")
+        _require(residual is None or (residual.shape == x.shape and residual.dtype == x.dtype),
+                 "rmsnorm: residual must match x")
         if residual is None:
             return _RMSNorm.apply(x.contiguous(), w.contiguous(), eps, None), x
         return _RMSNorm.apply(x.contiguous(), w.contiguous(), eps, residual.contiguous())
@@ -100,6 +113,8 @@ class _SwiGLU(torch.autograd.Function):
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
     """silu(gu[..., :F]) * gu[..., F:]"""
     if use_hip(gu):
+        _require(gu.dtype == torch.bfloat16 and gu.shape[-1] % 16 == 0,
+                 "swiglu: gu must be bf16 [..., 2F] with F % 8 == 0")
         return _SwiGLU.apply(gu.contiguous())
     Fh = gu.shape[-1] // 2
     return ref.swiglu(gu[..., :Fh], gu[..., Fh:])
@@ -141,6 +156,17 @@ def rope_qkv(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, seq_len: i
              hq: int, hkv: int, d: int):
     """qkv [T, (hq+2hkv)d] -> q [T,hq,d], k [T,hkv,d], v [T,hkv,d] (rotated q, k)."""
     if use_hip(qkv):
+        # Host-side operand checks: the kernel indexes cos/sin as fp32 [S, d/2]
+        # rows by (row % S) and reads qkv rows of (hq+2hkv)*d bf16.
+        _require(qkv.dtype == torch.bfloat16 and qkv.dim() == 2
+                 and qkv.shape[1] == (hq + 2 * hkv) * d, "rope: qkv must be bf16 [T, (hq+2hkv)*d]")
+        _require(d % 16 == 0, "rope: head_dim must be a multiple of 16")
+        _require(qkv.shape[0] % seq_len == 0, "rope: T must be a multiple of seq_len")
+        cos = cos.to(torch.float32).contiguous()
+        sin = sin.to(torch.float32).contiguous()
+        _require(cos.shape == sin.shape and cos.dim() == 2 and cos.shape[0] >= seq_len
+                 and cos.shape[1] == d // 2 and cos.device == qkv.device,
+                 "rope: cos/sin must be fp32 [>=S, d/2] on the qkv device")
         return _RopeQKV.apply(qkv.contiguous(), cos, sin, seq_len, hq, hkv, d)
     return ref.rope_qkv(qkv, cos, sin, seq_len, hq, hkv, d)
 
@@ -177,7 +203,10 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
     logits = logits.reshape(-1, logits.shape[-1])
     labels = labels.reshape(-1)
     if use_hip(logits):
-        assert logits.shape[-1] % 8 == 0, "vocab must be a multiple of 8 (16-B rows)"
+        _require(logits.dtype == torch.bfloat16 and logits.shape[-1] % 8 == 0,
+                 "cross_entropy: logits must be bf16 with vocab % 8 == 0 (16-B rows)")
+        _require(labels.numel() == logits.shape[0] and labels.device == logits.device,
+                 "cross_entropy: one label per logits row, same device")
         return _CrossEntropy.apply(logits.contiguous(), labels.to(torch.int64).contiguous(),
                                    ignore_index)
     return ref.cross_entropy(logits, labels, ignore_index)

@@ -151,3 +151,34 @@ def test_llama_tiny_train_step_hip():
     l_gpu.backward()
     for n, p in m_gpu.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad.float()).all(), n
+
+
+def test_rope_rejects_out_of_contract_tables():
+    """bf16 tables (e.g. cast by an FSDP MixedPrecisionPolicy) are converted,
+    too-short tables are rejected on the host before any launch."""
+    qkv = torch.randn(2 * 64, 8 * 128, device=DEV, dtype=torch.bfloat16)
+    cos, sin = ref.rope_tables(64, 128, 500000.0, DEV)
+    q1, _, _ = K.rope_qkv(qkv, cos.bfloat16(), sin.bfloat16(), 64, 4, 2, 128)
+    q2, _, _ = K.rope_qkv(qkv, cos, sin, 64, 4, 2, 128)
+    assert (q1.float() - q2.float()).abs().max().item() < 0.1
+    with pytest.raises(ValueError):
+        K.rope_qkv(qkv, cos[:10], sin[:10], 64, 4, 2, 128)
+
+
+def test_fsdp2_single_rank_train_step():
+    """The exact path bench.py runs: FSDP2 (1 rank, RCCL) + bf16 mixed precision
+    + HIP ops + fused AdamW."""
+    import torch.distributed as dist
+
+    from kgwe.bench.train import TrainConfig, Trainer
+    from kgwe.parallel import dist as kd
+
+    info = kd.init(force_group=True)
+    try:
+        tr = Trainer(TrainConfig(model="tiny", seq_len=256, micro_batch=2), info)
+        losses = [tr.step().item() for _ in range(3)]
+        assert all(torch.isfinite(torch.tensor(losses)))
+        assert losses[-1] < losses[0]
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()

@@ -1,0 +1,97 @@
+"""MI355X partition controller (MIG replacement) and GPU sharing manager."""
+import pytest
+
+from kgwe.core import Platform, make_fixture
+
+
+def part_wl(uid, mode="CPX", count=1):
+    return {"metadata": {"name": uid, "namespace": "inf", "uid": uid},
+            "spec": {"workloadType": "Inference",
+                     "gpuRequirements": {"count": 0, "partition": {"mode": mode, "count": count}}}}
+
+
+@pytest.fixture
+def plat():
+    p = Platform({})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    return p
+
+
+def test_cpx_one_gpu_split_eight_ways_binpacks_eight_pods(plat):
+    # BASELINE config 4: one GPU split 8-way, 8 inference pods bin-packed.
+    decisions = [plat.schedule(part_wl(f"inf{i}")) for i in range(8)]
+    assert all(d["ok"] for d in decisions)
+    gpus = {d["partitions"][0].rsplit("/p", 1)[0] for d in decisions}
+    assert len(gpus) == 1, "all 8 slices must come from ONE GPU (bin-packing)"
+    assert len({d["partitions"][0] for d in decisions}) == 8
+    assert plat.fake_partition_switches("n0") == 1
+    m = plat.partition_metrics()
+    assert m["modes"]["CPX"]["slices_in_use"] == 8 and m["slice_utilization"] == 1.0
+    # CPX slice env: logical HIP device = GPU base + slice index
+    envs = sorted(int(d["env"]["HIP_VISIBLE_DEVICES"]) for d in decisions)
+    assert envs == list(range(min(envs), min(envs) + 8))
+
+
+def test_ninth_pod_converts_a_second_gpu(plat):
+    for i in range(9):
+        assert plat.schedule(part_wl(f"p{i}"))["ok"]
+    assert plat.fake_partition_switches("n0") == 2
+
+
+def test_busy_gpu_never_repartitioned(plat):
+    whole = plat.schedule({"metadata": {"name": "t", "uid": "t"},
+                           "spec": {"gpuRequirements": {"count": 8}}})
+    assert whole["ok"]
+    d = plat.schedule(part_wl("x"))
+    assert not d["ok"]
+    assert plat.fake_partition_switches("n0") == 0
+
+
+def test_strategy_validation_and_rebalance(plat):
+    bad = {"metadata": {"name": "bad"}, "spec": {"profileDistribution": {"CPX": 0.8, "QPX": 0.5}}}
+    assert "sums to more" in plat.register_strategy(bad)
+    tpx = {"metadata": {"name": "tpx"}, "spec": {"profileDistribution": {"TPX": 0.5}}}
+    assert "TPX" in plat.register_strategy(tpx)
+    good = {"metadata": {"name": "mix"},
+            "spec": {"profileDistribution": {"CPX": 0.25, "QPX": 0.25}, "rebalanceInterval": "5m"}}
+    assert plat.register_strategy(good) == ""
+    plan = plat.rebalance("mix", plan_only=True)
+    assert len(plan) == 4 and plat.fake_partition_switches("n0") == 0
+    ops = plat.rebalance("mix")
+    assert all(o["state"] == "Completed" for o in ops)
+    modes = [g["partition"]["compute"] for g in plat.node("n0")["gpus"]]
+    assert modes.count("CPX") == 2 and modes.count("QPX") == 2 and modes.count("SPX") == 4
+
+
+def test_reclaim_idle_partitioned_gpus(plat):
+    plat.ensure_partitions("CPX", 8)
+    assert plat.partition_metrics()["modes"]["CPX"]["gpus"] == 1
+    ops = plat.reclaim_idle_partitions()
+    assert len(ops) == 1
+    assert "CPX" not in plat.partition_metrics()["modes"]
+
+
+def test_dry_run_does_not_actuate():
+    p = Platform({"partitionDryRun": True})
+    p.add_fake_node(make_fixture("d0", 8, 2))
+    ops = p.ensure_partitions("CPX", 8)
+    assert ops and ops[0]["dry_run"] and p.fake_partition_switches("d0") == 0
+
+
+def test_colocation_gets_disjoint_cu_masks(plat):
+    g = "GPU-n0-00"
+    a = plat.share_allocate({"uid": "a", "node": "n0", "gpu": g, "cuPercent": 25, "memoryGB": 40})
+    b = plat.share_allocate({"uid": "b", "node": "n0", "gpu": g, "cuPercent": 50, "memoryGB": 40})
+    assert a["error"] == "" and b["error"] == ""
+    assert a["method"] == "CoLocate"
+    assert a["env"]["HSA_CU_MASK"] == "0:0-63" and b["env"]["HSA_CU_MASK"] == "0:64-191"
+    c = plat.share_allocate({"uid": "c", "node": "n0", "gpu": g, "cuPercent": 50})
+    assert "compute units" in c["error"]
+    assert plat.share_release("a")
+    c = plat.share_allocate({"uid": "c", "node": "n0", "gpu": g, "cuPercent": 25})
+    assert c["error"] == "" and c["cu_begin"] == 0
+
+
+def test_sharing_method_selection(plat):
+    r = plat.share_allocate({"uid": "iso", "requireIsolation": True, "gpu": "GPU-n0-01"})
+    assert r["method"] == "Partition"
