@@ -50,8 +50,7 @@ class _RMSNorm(torch.autograd.Function):
         dy2 = dy.reshape(-1, H).contiguous()
         dadd = dh.reshape(-1, H).contiguous() if dh is not None else None
         dx = torch.empty_like(dy2)
-        G = lib().kgwe_rmsnorm_bwd_grid(T)
-        partial = torch.empty(G, H, device=h.device, dtype=torch.float32)
+        partial = torch.empty(H, device=h.device, dtype=torch.float32)  # dw accumulator
         dw = torch.empty(H, device=h.device, dtype=w.dtype)
         dw_bf = dw if w.dtype == torch.bfloat16 else None
         dw_f = dw if w.dtype == torch.float32 else None
