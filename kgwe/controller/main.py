@@ -1,0 +1,102 @@
+"""kgwe-controller: one process serving the whole control plane.
+
+* :8080  kube-scheduler extender (/filter /prioritize /bind), admission webhook
+         (/validate /mutate), node-agent push (/v1/nodes/<name>/topology),
+         /metrics, /healthz, /debug/*  (reference D1: Dockerfile.controller
+         8080/8443, scheduler-configmap.yaml:62)
+* reconcile loops for GPUWorkload / GPUBudget / PartitionStrategy
+* optional optimizer gRPC client (:50051) for placement hints
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import signal
+import threading
+import time
+
+from ..api import webhook
+from ..core import Platform, make_fixture
+from ..extender.server import ExtenderServer
+from ..utils.config import load_config
+from .kube import KubeClient
+from .reconciler import Reconciler
+
+DEFAULTS = {
+    "listen": {"host": "0.0.0.0", "port": 8080, "urlPrefix": ""},
+    "kube": {"url": "", "inCluster": False, "insecure": False},
+    "scheduler": {"topologyWeight": 40, "resourceWeight": 35, "balanceWeight": 25,
+                  "enablePreemption": True, "enableGangScheduling": True, "gangTimeoutMs": 30000,
+                  "maxSchedulingAttempts": 3, "scoring": "xgmi"},
+    "cost": {"journalPath": "", "enableSpotOptimization": True, "enableRightsizing": True},
+    "partitionDryRun": False,
+    "autoProvisionPartitions": True,
+    "enforceBudgets": True,
+    "optimizer": {"target": ""},
+    "fakeNodes": 0,
+    "tickSeconds": 5.0,
+}
+
+
+def build(cfg: dict):
+    plat = Platform({k: cfg[k] for k in ("scheduler", "cost", "partitionDryRun",
+                                         "autoProvisionPartitions", "enforceBudgets")})
+    for i in range(int(cfg.get("fakeNodes", 0))):
+        plat.add_fake_node(make_fixture(f"mi355x-sim-{i:03d}", 8, 2))
+    kube = None
+    if cfg["kube"]["inCluster"]:
+        kube = KubeClient.in_cluster()
+    elif cfg["kube"]["url"]:
+        kube = KubeClient(cfg["kube"]["url"], insecure=cfg["kube"]["insecure"])
+
+    def agent_push(path, body):
+        node = json.loads(body)
+        name = path.rstrip("/").split("/")[-2]  # /v1/nodes/<name>/topology
+        node["name"] = name
+        plat.upsert_node(node)
+        return 200, b'{"ok":true}'
+
+    def admission(path, body):
+        return 200, json.dumps(webhook.review(json.loads(body), mutate=path.startswith("/mutate"))).encode()
+
+    ext = ExtenderServer(plat, kube=kube, host=cfg["listen"]["host"], port=int(cfg["listen"]["port"]),
+                         url_prefix=cfg["listen"]["urlPrefix"],
+                         routes={"/v1/nodes/": agent_push, "/validate": admission, "/mutate": admission})
+    optimizer = None
+    if cfg["optimizer"]["target"]:
+        from ..optimizer.server import OptimizerClient  # noqa: PLC0415
+
+        client = OptimizerClient(cfg["optimizer"]["target"])
+        optimizer = type("Opt", (), {"GetPlacement": lambda self, r: client.call("GetPlacement", r)})()
+    rec = Reconciler(plat, kube, optimizer=optimizer, tick_s=float(cfg["tickSeconds"])) if kube else None
+    return plat, ext, rec
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="kgwe controller")
+    ap.add_argument("--config", help="YAML config file")
+    ap.add_argument("--set", action="append", default=[], help="override key.path=value")
+    a = ap.parse_args(argv)
+    cfg = load_config(DEFAULTS, a.config, a.set, env_prefix="KGWE_CONTROLLER_")
+    plat, ext, rec = build(cfg)
+    ext.start()
+    if rec:
+        rec.start()
+    print(f"kgwe-controller listening on {ext.url} (restored {rec.restored if rec else 0} allocations)",
+          flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    try:
+        while not stop.wait(1.0):
+            if rec is None:
+                plat.tick(time.time())
+    except KeyboardInterrupt:
+        pass
+    if rec:
+        rec.stop()
+    ext.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,314 @@
+"""Controller reconcile loops for GPUWorkload / GPUBudget / PartitionStrategy.
+
+Reference: the designed flow (docs/architecture.md:139-168) —
+"[controller] reconciles CR -> creates Pod(schedulerName=kgwe-scheduler,
+podTemplate)", writes GPUWorkload.status, starts/stops cost tracking — none of
+which exists in the reference (D1).  Here:
+
+* GPUWorkload -> one Pod per workload (podTemplate + schedulerName
+  ``kgwe-scheduler`` + amd.com/gpu or amd.com/gpu-<mode> limits + the spec as
+  the ``kgwe.amd.com/workload`` annotation the extender parses) -> status
+  (phase, node, GPUs / slices, score, estimated xGMI bandwidth, RCCL env,
+  conditions, start/completion time, cost).
+* Pod termination / deletion -> allocation release + cost finalisation.
+* GPUBudget -> cost-engine budget; status (spend, utilisation, alerts).
+* PartitionStrategy -> registered + rebalanced every rebalanceInterval.
+* Restart safety (checkpoint/resume): on start the ledger is
+  rebuilt from the allocation annotations of already-bound pods, so a
+  controller restart neither leaks nor double-allocates GPUs.
+"""
+from __future__ import annotations
+
+import json
+import threading
+import time
+from datetime import datetime, timezone
+
+from ..api import crds
+from ..extender.server import ANN_BW, ANN_ENV, ANN_GPUS, ANN_NODE, ANN_PARTS, ANN_SCORE
+from .kube import ApiError, KubeClient
+from .schedsim import SCHEDULER_NAME
+
+ANN_WORKLOAD = "kgwe.amd.com/workload"
+LABEL_WORKLOAD = "kgwe.amd.com/gpuworkload"
+
+
+def _now_iso() -> str:
+    return datetime.now(timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+def pod_for_workload(gw: dict) -> dict:
+    md = gw["metadata"]
+    spec = gw["spec"]
+    req = spec["gpuRequirements"]
+    tmpl = json.loads(json.dumps(spec.get("podTemplate") or {}))
+    pod_spec = tmpl.get("spec") or {"containers": [{"name": "main", "image": "rocm/pytorch:latest"}]}
+    pod_spec["schedulerName"] = SCHEDULER_NAME
+    pod_spec.setdefault("restartPolicy", "Never")
+    if "priority" in spec:
+        pod_spec["priority"] = int(spec["priority"])
+    if req.get("partition"):
+        res = {f"amd.com/gpu-{req['partition']['mode'].lower()}": str(req["partition"].get("count", 1))}
+    else:
+        res = {"amd.com/gpu": str(req.get("count", 1))}
+    c0 = pod_spec["containers"][0]
+    lim = c0.setdefault("resources", {}).setdefault("limits", {})
+    lim.update(res)
+    # Downward API: kgwe.launch reads the placement annotations at start.
+    pod_spec.setdefault("volumes", []).append(
+        {"name": "kgwe-podinfo", "downwardAPI": {"items": [
+            {"path": "annotations", "fieldRef": {"fieldPath": "metadata.annotations"}}]}})
+    c0.setdefault("volumeMounts", []).append({"name": "kgwe-podinfo", "mountPath": "/etc/kgwe"})
+    labels = dict((tmpl.get("metadata") or {}).get("labels") or {})
+    labels[LABEL_WORKLOAD] = md["name"]
+    if spec.get("team"):
+        labels["kgwe.amd.com/team"] = spec["team"]
+    if spec.get("project"):
+        labels["kgwe.amd.com/project"] = spec["project"]
+    ann = dict((tmpl.get("metadata") or {}).get("annotations") or {})
+    ann[ANN_WORKLOAD] = json.dumps({"metadata": {"name": md["name"], "namespace": md.get("namespace", "default"),
+                                                 "labels": labels}, "spec": {k: v for k, v in spec.items()
+                                                                             if k != "podTemplate"}})
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": f"{md['name']}-gw", "namespace": md.get("namespace", "default"),
+                         "labels": labels, "annotations": ann,
+                         "ownerReferences": [{"apiVersion": f"{crds.GROUP}/{crds.VERSION}", "kind": "GPUWorkload",
+                                              "name": md["name"], "uid": md.get("uid", ""),
+                                              "controller": True}]},
+            "spec": pod_spec}
+
+
+class Reconciler:
+    def __init__(self, platform, kube: KubeClient, optimizer=None, tick_s: float = 5.0):
+        self.p = platform
+        self.kube = kube
+        self.optimizer = optimizer
+        self.tick_s = tick_s
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+        self._strategy_next: dict[str, float] = {}
+        self.restored = 0
+
+    # ------------------------------------------------------------- lifecycle
+    def start(self) -> "Reconciler":
+        self.restored = self.rebuild_ledger()
+        for fn in (self._watch_workloads, self._watch_pods, self._watch_budgets, self._watch_strategies,
+                   self._periodic):
+            t = threading.Thread(target=fn, daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    def rebuild_ledger(self) -> int:
+        """Restore allocations from bound pods' annotations (restart safety)."""
+        n = 0
+        try:
+            pods = self.kube.list_pods()
+        except Exception:  # noqa: BLE001
+            return 0
+        for pod in pods:
+            md = pod.get("metadata", {})
+            ann = md.get("annotations") or {}
+            node = pod.get("spec", {}).get("nodeName")
+            if not node or ANN_GPUS not in ann:
+                continue
+            if pod.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+                continue
+            alloc = {"uid": md.get("uid") or f"{md.get('namespace')}/{md.get('name')}", "node": node,
+                     "namespace": md.get("namespace", "default"),
+                     "team": (md.get("labels") or {}).get("kgwe.amd.com/team", ""),
+                     "gpus": [g for g in ann.get(ANN_GPUS, "").split(",") if g],
+                     "partitions": [p for p in ann.get(ANN_PARTS, "").split(",") if p],
+                     "priority": pod.get("spec", {}).get("priority", 0)}
+            if self.p.restore_allocation(alloc):
+                n += 1
+        return n
+
+    def _loop(self, path: str, handler):
+        rv = "0"
+        while not self._stop.is_set():
+            try:
+                evs, rv = self.kube.watch(path, rv, timeout_s=2)
+            except Exception:  # noqa: BLE001
+                time.sleep(0.2)
+                continue
+            for e in evs:
+                try:
+                    handler(e["type"], e["object"])
+                except Exception as ex:  # noqa: BLE001 - keep the loop alive, surface in status
+                    self._record_error(e.get("object", {}), ex)
+
+    def _record_error(self, obj: dict, ex: Exception):
+        md = obj.get("metadata", {})
+        if obj.get("kind") == "GPUWorkload":
+            try:
+                self.kube.patch_cr_status("GPUWorkload", md.get("namespace"), md.get("name"),
+                                          {"message": f"reconcile error: {ex}"})
+            except Exception:  # noqa: BLE001
+                pass
+
+    # ------------------------------------------------------------- GPUWorkload
+    def _watch_workloads(self):
+        self._loop(f"/apis/{crds.GROUP}/{crds.VERSION}/gpuworkloads", self.on_workload)
+
+    def on_workload(self, typ: str, gw: dict):
+        md = gw["metadata"]
+        ns, name = md.get("namespace", "default"), md["name"]
+        if typ == "DELETED":
+            self.kube.delete_pod(ns, f"{name}-gw")
+            return
+        if gw.get("status", {}).get("phase") in ("Scheduling", "Scheduled", "Running", "Succeeded", "Failed"):
+            return
+        gw = crds.default(gw)
+        errs = crds.validate(gw)
+        if errs:
+            self.kube.patch_cr_status("GPUWorkload", ns, name, {
+                "phase": "Failed", "message": "; ".join(errs),
+                "conditions": [{"type": "Valid", "status": "False", "reason": "Invalid",
+                                "message": "; ".join(errs), "lastTransitionTime": _now_iso()}]})
+            return
+        if self.optimizer is not None:  # optimizer hint -> +10 preferred-node bonus
+            try:
+                req = gw["spec"]["gpuRequirements"]
+                hint = self.optimizer.GetPlacement({"workload_id": md.get("uid", name),
+                                                    "cluster_topology": self.p.snapshot(),
+                                                    "requirements": {"gpu_count": req.get("count", 1),
+                                                                     "prefer_xgmi": True}})
+                if hint.get("preferred_nodes"):
+                    gw["spec"]["preferredNodes"] = hint["preferred_nodes"]
+            except Exception:  # noqa: BLE001 - the hint is optional
+                pass
+        pod = pod_for_workload(gw)
+        try:
+            self.kube.create_pod(pod)
+        except ApiError as e:
+            if e.status != 409:
+                raise
+        self.kube.patch_cr_status("GPUWorkload", ns, name, {
+            "phase": "Scheduling", "podName": pod["metadata"]["name"],
+            "conditions": [{"type": "PodCreated", "status": "True", "reason": "Created",
+                            "lastTransitionTime": _now_iso()}]})
+
+    # ------------------------------------------------------------- Pods
+    def _watch_pods(self):
+        self._loop("/api/v1/pods", self.on_pod)
+
+    def on_pod(self, typ: str, pod: dict):
+        md = pod.get("metadata", {})
+        wl = (md.get("labels") or {}).get(LABEL_WORKLOAD)
+        ns = md.get("namespace", "default")
+        uid = md.get("uid") or f"{ns}/{md.get('name')}"
+        phase = pod.get("status", {}).get("phase")
+        ann = md.get("annotations") or {}
+        if typ == "DELETED" or phase in ("Succeeded", "Failed"):
+            rel = self.p.release(uid)
+            if wl:
+                st = {"phase": "Failed" if phase == "Failed" else "Succeeded", "completionTime": _now_iso()}
+                cost = rel.get("cost")
+                if cost:
+                    st["cost"] = cost["adjusted_cost"]
+                try:
+                    self.kube.patch_cr_status("GPUWorkload", ns, wl, st)
+                except ApiError:
+                    pass
+            return
+        if wl and pod.get("spec", {}).get("nodeName") and ANN_GPUS in ann:
+            st = {"phase": "Running" if phase == "Running" else "Scheduled",
+                  "scheduledNode": ann.get(ANN_NODE) or pod["spec"]["nodeName"],
+                  "allocatedGPUs": [g for g in ann.get(ANN_GPUS, "").split(",") if g],
+                  "partitionSlices": [g for g in ann.get(ANN_PARTS, "").split(",") if g],
+                  "schedulingScore": int(ann.get(ANN_SCORE, "0") or 0),
+                  "estimatedBandwidth": float(ann.get(ANN_BW, "0") or 0),
+                  "rcclEnv": json.loads(ann.get(ANN_ENV, "{}")),
+                  "startTime": _now_iso(),
+                  "conditions": [{"type": "Scheduled", "status": "True", "reason": "Bound",
+                                  "lastTransitionTime": _now_iso()}]}
+            self.kube.patch_cr_status("GPUWorkload", ns, wl, st)
+
+    # ------------------------------------------------------------- GPUBudget
+    def _watch_budgets(self):
+        self._loop(f"/apis/{crds.GROUP}/{crds.VERSION}/gpubudgets", self.on_budget)
+
+    def on_budget(self, typ: str, b: dict):
+        if typ == "DELETED":
+            return
+        b = crds.default(b)
+        errs = crds.validate(b)
+        md = b["metadata"]
+        if errs:
+            self.kube.patch_cr_status("GPUBudget", md.get("namespace"), md["name"],
+                                      {"conditions": [{"type": "Valid", "status": "False",
+                                                       "message": "; ".join(errs)}]})
+            return
+        if typ == "ADDED" or "currentSpend" not in (b.get("status") or {}):
+            spec = dict(b["spec"])
+            if spec.get("scope", "Namespace") == "Namespace":
+                spec.setdefault("scopeId", md.get("namespace", "default"))
+            elif spec.get("scope") == "Team":
+                spec.setdefault("scopeId", spec.get("teamId", ""))
+            self.p.create_budget({"metadata": md, "spec": spec})
+
+    def _budget_status(self):
+        for b in self.p.budgets():
+            ns, _, name = b["id"].rpartition("/")
+            alerts = [a for a in self.p.alerts() if a["budget_id"] == b["id"]]
+            try:
+                self.kube.patch_cr_status("GPUBudget", ns or None, name, {
+                    "currentSpend": f"{b['spend']:.2f}", "utilizationPercent": round(b["utilization_percent"], 2),
+                    "periodStart": datetime.fromtimestamp(b["period_start_s"], timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+                    "periodEnd": datetime.fromtimestamp(b["period_end_s"], timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+                    "alerts": [{"severity": a["severity"], "threshold": a["threshold"], "message": a["message"]}
+                               for a in alerts[-10:]]})
+            except ApiError:
+                pass
+
+    # ------------------------------------------------------------- PartitionStrategy
+    def _watch_strategies(self):
+        self._loop(f"/apis/{crds.GROUP}/{crds.VERSION}/partitionstrategies", self.on_strategy)
+
+    def on_strategy(self, typ: str, s: dict):
+        name = s["metadata"]["name"]
+        if typ == "DELETED":
+            self._strategy_next.pop(name, None)
+            return
+        s = crds.default(s)
+        err = "; ".join(crds.validate(s)) or self.p.register_strategy(s)
+        if err:
+            self.kube.patch_cr_status("PartitionStrategy", None, name, {
+                "conditions": [{"type": "Valid", "status": "False", "message": err}]})
+            return
+        self._strategy_next[name] = 0.0  # rebalance at next tick
+
+    def _rebalance_due(self, now: float):
+        for st in self.p.strategies():
+            name = st["name"]
+            if name not in self._strategy_next or now < self._strategy_next[name]:
+                continue
+            ops = self.p.rebalance(name)
+            self._strategy_next[name] = now + max(1, st.get("rebalanceIntervalSeconds", 300))
+            dist: dict = {}
+            for g in (n for nd in self.p.snapshot()["nodes"].values() for n in nd["gpus"]):
+                dist[g["partition"]["compute"]] = dist.get(g["partition"]["compute"], 0) + 1
+            try:
+                self.kube.patch_cr_status("PartitionStrategy", None, name, {
+                    "lastRebalanceTime": _now_iso(), "currentDistribution": dist,
+                    "appliedNodes": sorted({o["node"] for o in ops}),
+                    "conditions": [{"type": "Rebalanced", "status": "True",
+                                    "message": f"{len(ops)} reconfiguration(s)"}]})
+            except ApiError:
+                pass
+
+    # ------------------------------------------------------------- periodic
+    def _periodic(self):
+        while not self._stop.wait(self.tick_s):
+            now = time.time()
+            try:
+                self.p.refresh_telemetry()
+                self.p.tick(now)
+                self._rebalance_due(now)
+                self._budget_status()
+            except Exception:  # noqa: BLE001
+                pass

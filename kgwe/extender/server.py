@@ -48,10 +48,14 @@ def _created_s(meta: dict) -> float | None:
 
 class ExtenderServer:
     def __init__(self, platform: Platform, kube=None, host: str = "0.0.0.0", port: int = 8080,
-                 url_prefix: str = ""):
+                 url_prefix: str = "", routes: dict | None = None):
+        """routes: extra POST handlers {path_prefix: fn(path, body) -> (code, bytes)}
+        (the controller mounts the admission webhook and the node-agent push
+        endpoint here)."""
         self.platform = platform
         self.kube = kube
         self.prefix = url_prefix.rstrip("/")
+        self.routes = dict(routes or {})
         self.tracer = tracing.PhaseTimer()
         outer = self
 
@@ -89,7 +93,15 @@ class ExtenderServer:
             def do_POST(self):
                 n = int(self.headers.get("Content-Length") or 0)
                 body = self.rfile.read(n).decode() if n else "{}"
-                verb = self.path.split("?")[0][len(outer.prefix):].strip("/")
+                path = self.path.split("?")[0]
+                for pre, fn in outer.routes.items():
+                    if path.startswith(pre):
+                        try:
+                            code, data = fn(path, body)
+                        except Exception as e:  # noqa: BLE001
+                            code, data = 500, json.dumps({"error": str(e)}).encode()
+                        return self._send(code, data)
+                verb = path[len(outer.prefix):].strip("/")
                 try:
                     if verb == "filter":
                         with outer.tracer.phase("filter"):

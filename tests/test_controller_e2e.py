@@ -1,0 +1,186 @@
+"""End-to-end on a fake cluster (BASELINE.json config 1): fake apiserver +
+controller (reconciler + extender + webhook) + kube-scheduler stand-in, all
+over real HTTP.  GPUWorkload -> Pod -> filter/prioritize/bind -> status with
+allocated GPUs and RCCL env -> completion -> release + cost; budgets;
+partition strategies; restart-safe ledger; admission webhook; config."""
+import base64
+import json
+import time
+
+import pytest
+
+from kgwe.api import crds, webhook
+from kgwe.controller.apiserver import FakeApiServer
+from kgwe.controller.kube import KubeClient
+from kgwe.controller.main import DEFAULTS, build
+from kgwe.controller.schedsim import SchedulerSim
+from kgwe.utils.config import ConfigError, load_config
+
+
+def wait_for(fn, timeout=10.0, every=0.05):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        v = fn()
+        if v:
+            return v
+        time.sleep(every)
+    raise AssertionError("condition not met in time")
+
+
+@pytest.fixture
+def cluster():
+    api = FakeApiServer().start()
+    kube = KubeClient(api.url)
+    for i in range(2):
+        api.add_node(f"mi355x-{i}")
+    cfg = load_config(DEFAULTS, sets=["listen.host=127.0.0.1", "listen.port=0", f"kube.url={api.url}",
+                                      "tickSeconds=0.2"])
+    plat, ext, rec = build(cfg)
+    from kgwe.core import make_fixture
+    for i in range(2):
+        plat.add_fake_node(make_fixture(f"mi355x-{i}", 8, 2))
+    ext.start()
+    rec.start()
+    sim = SchedulerSim(kube, ext.url).start()
+    yield api, kube, plat, ext, rec
+    sim.stop()
+    rec.stop()
+    ext.stop()
+    api.stop()
+
+
+def gw(name, count=8, **spec):
+    s = {"gpuRequirements": {"count": count, "topology": {"preference": "NVLinkOptimal"}},
+         "distributedConfig": {"strategy": "FSDP", "worldSize": count, "backend": "NCCL"},
+         "podTemplate": {"spec": {"containers": [{"name": "train", "image": "rocm/pytorch",
+                                                  "command": ["torchrun", "train.py"]}]}}}
+    s.update(spec)
+    return {"apiVersion": "kgwe.amd.com/v1", "kind": "GPUWorkload",
+            "metadata": {"name": name, "namespace": "ml"}, "spec": s}
+
+
+def test_gpuworkload_lifecycle(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr(gw("llama3-8b-fsdp"))
+    st = wait_for(lambda: (kube.get_cr("GPUWorkload", "ml", "llama3-8b-fsdp").get("status") or {})
+                  if (kube.get_cr("GPUWorkload", "ml", "llama3-8b-fsdp").get("status") or {}).get("phase")
+                  in ("Scheduled", "Running") else None)
+    assert len(st["allocatedGPUs"]) == 8 and st["scheduledNode"].startswith("mi355x-")
+    env = st["rcclEnv"]
+    assert env["WORLD_SIZE"] == "8" and env["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7"
+    assert env["TORCH_DISTRIBUTED_BACKEND"] == "nccl" and st["estimatedBandwidth"] > 100
+    pod = kube.get_pod("ml", "llama3-8b-fsdp-gw")
+    assert pod["spec"]["schedulerName"] == "kgwe-scheduler"
+    assert pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "8"
+    assert plat.scheduler_metrics()["allocated_gpus"] == 8
+    # completion -> release + cost + status
+    kube.patch_pod("ml", "llama3-8b-fsdp-gw", {"status": {"phase": "Succeeded"}})
+    wait_for(lambda: plat.scheduler_metrics()["allocated_gpus"] == 0)
+    done = wait_for(lambda: kube.get_cr("GPUWorkload", "ml", "llama3-8b-fsdp")["status"]
+                    if kube.get_cr("GPUWorkload", "ml", "llama3-8b-fsdp")["status"]["phase"] == "Succeeded"
+                    else None)
+    assert "completionTime" in done
+
+
+def test_partition_workloads_bin_pack(cluster):
+    api, kube, plat, ext, rec = cluster
+    for i in range(8):
+        kube.create_cr(gw(f"inf-{i}", count=0, workloadType="Inference",
+                          gpuRequirements={"count": 0, "partition": {"mode": "CPX", "count": 1}},
+                          distributedConfig={"backend": "RCCL"}))
+    wait_for(lambda: plat.scheduler_metrics()["allocated_partitions"] == 8, timeout=15)
+    slices = [a["partitions"][0] for a in plat.allocations()]
+    assert len({s.rsplit("/p", 1)[0] for s in slices}) == 1
+
+
+def test_invalid_workload_fails_with_condition(cluster):
+    api, kube, plat, ext, rec = cluster
+    bad = gw("bad", count=100)
+    kube.create_cr(bad)
+    st = wait_for(lambda: kube.get_cr("GPUWorkload", "ml", "bad").get("status"))
+    assert st["phase"] == "Failed" and "maximum" in st["message"]
+
+
+def test_budget_block_enforced_and_status(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr({"apiVersion": "kgwe.amd.com/v1", "kind": "GPUBudget",
+                    "metadata": {"name": "tiny", "namespace": "ml"},
+                    "spec": {"limit": "1", "enforcementPolicy": "Block"}})
+    wait_for(lambda: plat.budgets())
+    kube.create_cr(gw("blocked", count=8))
+    time.sleep(0.6)
+    assert plat.scheduler_metrics()["allocated_gpus"] == 0
+    st = wait_for(lambda: kube.get_cr("GPUBudget", "ml", "tiny").get("status"))
+    assert st["currentSpend"] == "0.00"
+
+
+def test_partition_strategy_rebalanced(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr({"apiVersion": "kgwe.amd.com/v1", "kind": "PartitionStrategy",
+                    "metadata": {"name": "mixed"},
+                    "spec": {"profileDistribution": {"CPX": 0.25}, "rebalanceInterval": "5m"}})
+    st = wait_for(lambda: kube.get_cr("PartitionStrategy", None, "mixed").get("status"), timeout=5)
+    assert st["currentDistribution"].get("CPX") == 4
+
+
+def test_restart_rebuilds_ledger(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr(gw("persist", count=4))
+    wait_for(lambda: plat.scheduler_metrics()["allocated_gpus"] == 4)
+    cfg = load_config(DEFAULTS, sets=["listen.host=127.0.0.1", "listen.port=0", f"kube.url={api.url}"])
+    plat2, ext2, rec2 = build(cfg)
+    from kgwe.core import make_fixture
+    for i in range(2):
+        plat2.add_fake_node(make_fixture(f"mi355x-{i}", 8, 2))
+    assert rec2.rebuild_ledger() == 1
+    assert plat2.scheduler_metrics()["allocated_gpus"] == 4
+    ext2.httpd.server_close()
+
+
+def test_agent_push_endpoint(cluster):
+    import http.client
+    api, kube, plat, ext, rec = cluster
+    from kgwe.core import make_fixture
+    node = make_fixture("pushed", 8, 2)
+    h, p = ext.httpd.server_address[:2]
+    c = http.client.HTTPConnection(h, p)
+    c.request("POST", "/v1/nodes/pushed/topology", body=json.dumps(node))
+    assert c.getresponse().status == 200
+    assert plat.node("pushed")["name"] == "pushed"
+
+
+def test_webhook_mutates_and_validates():
+    obj = gw("w", count=2, gpuRequirements={"count": 0, "mig": {"profile": "1g.10gb", "count": 2}})
+    ar = {"request": {"uid": "u1", "operation": "CREATE", "object": obj}}
+    out = webhook.review(ar, mutate=True)["response"]
+    assert out["allowed"] and out["patchType"] == "JSONPatch"
+    patch = json.loads(base64.b64decode(out["patch"]))
+    spec = patch[0]["value"]
+    assert spec["gpuRequirements"]["partition"] == {"mode": "CPX", "count": 2, "memoryMode": "NPS1"}
+    assert spec["distributedConfig"]["backend"] == "RCCL"
+    bad = webhook.review({"request": {"uid": "u2", "operation": "CREATE",
+                                      "object": gw("x", count=65)}})["response"]
+    assert not bad["allowed"] and "maximum" in bad["status"]["message"]
+    both = gw("y", count=2, gpuRequirements={"count": 2, "partition": {"mode": "CPX"}})
+    assert any("not both" in e for e in crds.validate(both))
+
+
+def test_crd_render(tmp_path):
+    import yaml
+    paths = crds.render(tmp_path)
+    assert len(paths) == 3
+    doc = yaml.safe_load(paths[0].read_text())
+    assert doc["spec"]["group"] == "kgwe.amd.com"
+
+
+def test_config_rejects_unknown_keys(tmp_path):
+    with pytest.raises(ConfigError):
+        load_config(DEFAULTS, sets=["scheduler.noSuchKey=1"])
+    f = tmp_path / "c.yaml"
+    f.write_text("scheduler:\n  topologyWeight: 50\n")
+    cfg = load_config(DEFAULTS, str(f), environ={"KGWE_CONTROLLER_SCHEDULER__BALANCEWEIGHT": "10"},
+                      env_prefix="KGWE_CONTROLLER_")
+    assert cfg["scheduler"]["topologyWeight"] == 50 and cfg["scheduler"]["balanceWeight"] == 10
+    f.write_text("bogus: 1\n")
+    with pytest.raises(ConfigError):
+        load_config(DEFAULTS, str(f))
