@@ -318,8 +318,13 @@ def render(out_dir: str | Path) -> list[Path]:
     return paths
 
 
-if __name__ == "__main__":
-    target = sys.argv[1] if len(sys.argv) > 1 else "deploy/helm/kgwe-mi355x/crds"
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    target = argv[0] if argv else "deploy/helm/kgwe-mi355x/crds"
     for p in render(target):
         print(p)
-    json.dumps(KINDS["GPUWorkload"]["spec"])  # schema is JSON-serialisable
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -101,6 +101,17 @@ PYBIND11_MODULE(_kgwe_core, m) {
     return j.dump();
   }, py::arg("node") = "local", py::call_guard<py::gil_scoped_release>());
 
+  m.def("amdsmi_set_partition", [](const std::string& gpu, const std::string& compute,
+                                   const std::string& memory) {
+    AmdSmiHal h;
+    if (!h.ok()) return std::string("amd-smi unavailable: ") + h.error();
+    std::string err;
+    if (!memory.empty()) err = h.set_memory_partition(gpu, memory_partition_from(memory));
+    if (err.empty() && !compute.empty()) err = h.set_compute_partition(gpu, compute_partition_from(compute));
+    return err;
+  }, py::arg("gpu"), py::arg("compute"), py::arg("memory") = "",
+     py::call_guard<py::gil_scoped_release>());
+
   m.def("workload_from_pod", [](const std::string& pod) {
     return to_json(workload_from_pod(Json::parse(pod))).dump();
   });

@@ -1,0 +1,76 @@
+"""Node agent (fixture backend, push to controller, exporter), the container
+launcher, and the GPU-side probes / RCCL sweep (gpu-marked)."""
+import http.client
+import json
+
+import pytest
+
+from kgwe.agent.agent import DEFAULTS, NodeAgent
+from kgwe.core import Platform, make_fixture
+from kgwe.extender.server import ExtenderServer
+from kgwe.launch import parse_downward_api, placement_env
+from kgwe.utils.config import load_config
+
+
+def test_agent_fixture_push_and_metrics(tmp_path):
+    fx = tmp_path / "node.json"
+    fx.write_text(json.dumps(make_fixture("whatever", 8, 2)))
+    plat = Platform({})
+
+    def push(path, body):
+        node = json.loads(body)
+        node["name"] = path.rstrip("/").split("/")[-2]
+        plat.upsert_node(node)
+        return 200, b"{}"
+    ext = ExtenderServer(plat, host="127.0.0.1", port=0, routes={"/v1/nodes/": push}).start()
+    cfg = load_config(DEFAULTS, sets=["nodeName=gpu-node-7", f"fixture={fx}", f"controllerUrl={ext.url}",
+                                      "listen.host=127.0.0.1", "listen.port=0"])
+    agent = NodeAgent(cfg)
+    # measured-probe merge: GPU 3 HBM at 50 % of the median -> Degraded
+    agent.probe_results = {"hbm": {i: {"copy_gbps": 6000.0 if i != 3 else 3000.0} for i in range(8)},
+                           "xgmi": [[0 if s == d else 150.0 for s in range(8)] for d in range(8)]}
+    node = agent.discover()
+    assert node["name"] == "gpu-node-7"
+    assert node["gpus"][3]["health"]["status"] == "Degraded"
+    assert node["gpus"][0]["links"][0]["measured_gbps"] == 150.0
+    assert agent.push()
+    assert plat.node("gpu-node-7")["gpus"][3]["health"]["status"] == "Degraded"
+    srv = agent.serve()
+    h, p = srv.server_address[:2]
+    c = http.client.HTTPConnection(h, p)
+    c.request("GET", "/metrics")
+    text = c.getresponse().read().decode()
+    assert 'kgwe_gpu_health_status{gpu_uuid="GPU-whatever-03",node="gpu-node-7"} 0.5' in text
+    assert 'kgwe_gpu_hbm_bandwidth_gbps' in text
+    c.request("POST", "/v1/partition", body=json.dumps({"gpu": "GPU-whatever-00", "compute": "CPX"}))
+    r = json.loads(c.getresponse().read())
+    assert r["dryRun"] is True
+    srv.shutdown()
+    ext.stop()
+
+
+def test_launch_env_from_downward_api():
+    env = {"HIP_VISIBLE_DEVICES": "0,1", "WORLD_SIZE": "2"}
+    text = ('kgwe.amd.com/node="n1"\n'
+            f'kgwe.amd.com/rccl-env={json.dumps(json.dumps(env))}\n')
+    ann = parse_downward_api(text)
+    assert ann["kgwe.amd.com/node"] == "n1"
+    assert placement_env(ann) == env
+
+
+@pytest.mark.gpu
+def test_agent_probes_on_gpu():
+    cfg = load_config(DEFAULTS, sets=["probe.bytesMB=512", "probe.iters=3"])
+    agent = NodeAgent(cfg)
+    res = agent.run_probes()
+    assert res["devices"] >= 1
+    assert res["hbm"][0]["copy_gbps"] > 2000
+
+
+@pytest.mark.gpu
+def test_rccl_native_sweep_single_gpu():
+    from kgwe.parallel.busbw import native_sweep
+
+    r = native_sweep(1, sizes=[1 << 20, 1 << 24], iters=5)
+    assert r["ndev"] == 1 and len(r["rows"]) == 2
+    assert all(row["us"] > 0 for row in r["rows"])
