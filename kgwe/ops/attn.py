@@ -58,7 +58,21 @@ def set_force_sdpa(flag: bool) -> None:
 
 
 def hip_flash_available() -> bool:
-    return has_symbol("kgwe_flash_attn_fwd")
+    return has_symbol("kgwe_flash_attn_fwd") and has_symbol("kgwe_flash_attn_bwd")
+
+
+def flash_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True):
+    """Forward only (inference / tests): returns (o, lse2) with lse2 in log2 units."""
+    B, S, Hq, D = q.shape
+    if not (q.is_contiguous() and k.is_contiguous() and v.is_contiguous()
+            and q.dtype == k.dtype == v.dtype == torch.bfloat16 and D == 128
+            and k.shape == v.shape == (B, S, k.shape[2], D) and Hq % k.shape[2] == 0):
+        raise ValueError("flash_fwd: contiguous bf16 [B,S,H,128] q/k/v with Hq % Hkv == 0")
+    o = torch.empty_like(q)
+    lse = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+    check(lib().kgwe_flash_attn_fwd(ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, S, Hq, k.shape[2],
+                                    D, 1.0 / math.sqrt(D), int(causal), stream(q)), "flash_attn_fwd")
+    return o, lse
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True):
