@@ -32,3 +32,24 @@ def test_flash_fwd_matches_reference(B, S, Hq, Hkv, causal):
         s = s.masked_fill(torch.ones(S, S, device="cuda", dtype=torch.bool).triu(1), float("-inf"))
     lse_ref = torch.logsumexp(s, dim=-1) / math.log(2)
     assert (lse2 - lse_ref).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
+    (1, 128, 4, 4, True), (2, 256, 8, 2, True), (1, 512, 8, 2, True), (1, 256, 4, 1, False),
+    (1, 200, 4, 2, True)])
+def test_flash_bwd_matches_reference(B, S, Hq, Hkv, causal):
+    q, k, v = _inputs(B, S, Hq, Hkv, seed=1)
+    qh, kh, vh = (t.clone().requires_grad_(True) for t in (q, k, v))
+    o = attn._FlashAttn.apply(qh, kh, vh, causal)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    o_ref = ref.attention(qr, kr, vr, causal)
+    o_ref.backward(do.float())
+    for name, a, b in (("dq", qh.grad, qr.grad), ("dk", kh.grad, kr.grad), ("dv", vh.grad, vr.grad)):
+        rel = ((a.float() - b).norm() / b.norm()).item()
+        assert rel < 2e-2, (name, rel)
+
+
+def test_model_uses_hip_flash_attention():
+    assert attn.hip_flash_available()
