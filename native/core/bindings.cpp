@@ -29,6 +29,7 @@ PlatformConfig config_from_json(const std::string& s) {
   c.sched.max_attempts = static_cast<int>(sc.get("maxSchedulingAttempts").as_int(c.sched.max_attempts));
   c.sched.mode = sc.get("scoring").str("xgmi") == "compat" ? ScoringMode::Compat : ScoringMode::Xgmi;
   c.sched.rated_link_gbps = sc.get("ratedLinkGBps").as_number(c.sched.rated_link_gbps);
+  c.sched.pack = sc.get("placement").str("pack") != "spread";
   const Json& cc = j.get("cost");
   c.cost.journal_path = cc.get("journalPath").str();
   c.cost.enable_spot = cc.get("enableSpotOptimization").as_bool(true);

@@ -706,7 +706,7 @@ int Scheduler::resource_score(const std::vector<const GpuDevice*>& avail,
   return std::min(100, score);
 }
 
-int Scheduler::balance_score(const NodeTopology& n) const {
+int Scheduler::balance_score(const NodeTopology& n, int requested) const {
   if (n.gpus.empty()) return 0;
   double used;
   if (cfg_.mode == ScoringMode::Compat) {
@@ -716,6 +716,12 @@ int Scheduler::balance_score(const NodeTopology& n) const {
   } else {
     auto it = node_gpus_used_.find(n.name);
     used = it == node_gpus_used_.end() ? 0 : it->second;
+  }
+  if (cfg_.mode != ScoringMode::Compat && cfg_.pack) {
+    // Best fit across nodes: prefer the node that is fullest AFTER this
+    // placement, so whole 8-GPU xGMI islands stay free for FSDP/TP jobs
+    // (spreading small jobs fragments every node and makes 8-GPU jobs wait).
+    return std::min(100, static_cast<int>(100.0 * (used + requested) / n.gpus.size()));
   }
   return std::max(0, static_cast<int>(100.0 * (1.0 - used / n.gpus.size())));
 }
@@ -759,7 +765,7 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
       if (g.partition.compute == w.partition_mode) total_slices += static_cast<int>(g.partition.instances.size());
     s.topology = 100;
     s.resource = 50 + (total_slices ? 50 * used_slices / total_slices : 0);  // packing
-    s.balance = balance_score(n);
+    s.balance = balance_score(n, 0);
   } else {
     auto avail = free_gpus(n, w);
     if (static_cast<int>(avail.size()) < w.gpu_count) return s;
@@ -771,7 +777,7 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
       s.topology = topology_score(n, avail, w, &s.gpus, &s.bandwidth_gbps, &clique);
     }
     s.resource = resource_score(avail, w);
-    s.balance = balance_score(n);
+    s.balance = balance_score(n, w.gpu_count);
   }
   s.total = (s.topology * cfg_.topology_weight + s.resource * cfg_.resource_weight +
              s.balance * cfg_.balance_weight) / 100;

@@ -147,6 +147,7 @@ struct SchedulerConfig {
   int gang_timeout_ms = 30000;
   int max_attempts = 3;           // nodes tried best-first per Schedule
   ScoringMode mode = ScoringMode::Xgmi;
+  bool pack = true;                // xGMI mode: best-fit across nodes (false = spread)
   double rated_link_gbps = 153.6;  // MI355X xGMI per-link (normalisation)
   double degraded_link_ratio = 0.7;  // measured/rated below this => degraded link
   size_t event_capacity = 4096;
@@ -220,7 +221,7 @@ class Scheduler {
   int topology_score_compat(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
                             const WorkloadRequest& w, std::vector<std::string>* sel) const;
   int resource_score(const std::vector<const GpuDevice*>& avail, const WorkloadRequest& w) const;
-  int balance_score(const NodeTopology& n) const;
+  int balance_score(const NodeTopology& n, int requested) const;
   bool reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending);
   bool try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d);
   void emit(SchedEvent e);
