@@ -107,6 +107,8 @@ _CORE = re.compile(r"^/api/v1(?:/namespaces/(?P<ns>[^/]+))?/(?P<coll>nodes|pods|
                    r"(?:/(?P<name>[^/]+))?(?:/(?P<sub>binding|status))?$")
 _CRD = re.compile(r"^/apis/kgwe\.amd\.com/v1(?:/namespaces/(?P<ns>[^/]+))?/(?P<coll>gpuworkloads|"
                   r"partitionstrategies|gpubudgets)(?:/(?P<name>[^/]+))?(?:/(?P<sub>status))?$")
+_LEASE = re.compile(r"^/apis/coordination\.k8s\.io/v1/namespaces/(?P<ns>[^/]+)/(?P<coll>leases)"
+                    r"(?:/(?P<name>[^/]+))?(?P<sub>)$")
 
 
 class _Handler(BaseHTTPRequestHandler):
@@ -132,10 +134,11 @@ class _Handler(BaseHTTPRequestHandler):
     def _route(self):
         path, _, q = self.path.partition("?")
         qs = dict(p.split("=", 1) for p in q.split("&") if "=" in p)
-        m = _CORE.match(path) or _CRD.match(path)
+        m = _CORE.match(path) or _CRD.match(path) or _LEASE.match(path)
         if not m:
             return None, qs
         d = m.groupdict()
+        d["sub"] = d.get("sub") or None
         if d["coll"] == "nodes" or d["coll"] == "partitionstrategies":
             d["ns"] = None
         return d, qs
@@ -188,7 +191,28 @@ class _Handler(BaseHTTPRequestHandler):
         o = self.store.patch(d["coll"], d["ns"], d["name"], self._body())
         return self._send(200, o) if o else self._send(404, {"reason": "NotFound"})
 
-    do_PUT = do_PATCH
+    def do_PUT(self):
+        """Replace with optimistic concurrency: a stale metadata.resourceVersion
+        gets 409 Conflict (what leader election relies on)."""
+        d, _ = self._route()
+        if d is None or not d["name"]:
+            return self._send(404, {"message": "not found"})
+        body = self._body()
+        st = self.store
+        with st.lock:
+            cur = st.objs.get((d["coll"], d["ns"], d["name"]))
+            if cur is None:
+                return self._send(404, {"reason": "NotFound"})
+            want = body.get("metadata", {}).get("resourceVersion")
+            if want and want != cur["metadata"].get("resourceVersion"):
+                return self._send(409, {"reason": "Conflict"})
+            body.setdefault("metadata", {})
+            for k in ("uid", "creationTimestamp", "namespace", "name"):
+                if k in cur["metadata"]:
+                    body["metadata"][k] = cur["metadata"][k]
+            st.objs[(d["coll"], d["ns"], d["name"])] = body
+            st._bump(d["coll"], "MODIFIED", body)
+            return self._send(200, copy.deepcopy(body))
 
     def do_DELETE(self):
         d, _ = self._route()

@@ -27,7 +27,8 @@ DEFAULTS = {
     "kube": {"url": "", "inCluster": False, "insecure": False},
     "scheduler": {"topologyWeight": 40, "resourceWeight": 35, "balanceWeight": 25,
                   "enablePreemption": True, "enableGangScheduling": True, "gangTimeoutMs": 30000,
-                  "maxSchedulingAttempts": 3, "scoring": "xgmi"},
+                  "maxSchedulingAttempts": 3, "scoring": "xgmi", "placement": "pack"},
+    "webhook": {"port": 8443, "certFile": "", "keyFile": ""},
     "cost": {"journalPath": "", "enableSpotOptimization": True, "enableRightsizing": True},
     "partitionDryRun": False,
     "autoProvisionPartitions": True,
@@ -35,6 +36,8 @@ DEFAULTS = {
     "optimizer": {"target": ""},
     "fakeNodes": 0,
     "tickSeconds": 5.0,
+    "leaderElection": {"enabled": True, "namespace": "kube-system", "leaseName": "kgwe-controller",
+                       "identity": "", "leaseSeconds": 15.0, "renewSeconds": 10.0, "retrySeconds": 2.0},
 }
 
 
@@ -79,11 +82,26 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     cfg = load_config(DEFAULTS, a.config, a.set, env_prefix="KGWE_CONTROLLER_")
     plat, ext, rec = build(cfg)
+    wh = cfg["webhook"]
+    if wh["certFile"]:
+        ext.add_tls_listener(cfg["listen"]["host"], int(wh["port"]), wh["certFile"], wh["keyFile"])
     ext.start()
-    if rec:
+    elector = None
+    le = cfg["leaderElection"]
+    if rec and le["enabled"]:
+        import os  # noqa: PLC0415
+        import socket  # noqa: PLC0415
+
+        from .leader import LeaderElector  # noqa: PLC0415
+
+        ident = le["identity"] or f"{socket.gethostname()}-{os.getpid()}"
+        elector = LeaderElector(rec.kube, le["leaseName"], ident, le["namespace"], le["leaseSeconds"],
+                                le["renewSeconds"], le["retrySeconds"], on_started=rec.start,
+                                on_stopped=rec.stop).start()
+        ext.ready = lambda: elector.is_leader
+    elif rec:
         rec.start()
-    print(f"kgwe-controller listening on {ext.url} (restored {rec.restored if rec else 0} allocations)",
-          flush=True)
+    print(f"kgwe-controller listening on {ext.url}", flush=True)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     try:
@@ -92,6 +110,8 @@ def main(argv=None) -> int:
                 plat.tick(time.time())
     except KeyboardInterrupt:
         pass
+    if elector:
+        elector.stop()
     if rec:
         rec.stop()
     ext.stop()

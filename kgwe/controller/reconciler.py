@@ -91,6 +91,10 @@ class Reconciler:
 
     # ------------------------------------------------------------- lifecycle
     def start(self) -> "Reconciler":
+        """(Re)start — also called by the leader elector on every takeover: the
+        new leader first rebuilds the ledger from the apiserver."""
+        self._stop.clear()
+        self._threads = []
         self.restored = self.rebuild_ledger()
         for fn in (self._watch_workloads, self._watch_pods, self._watch_budgets, self._watch_strategies,
                    self._periodic):

@@ -56,6 +56,7 @@ class ExtenderServer:
         self.kube = kube
         self.prefix = url_prefix.rstrip("/")
         self.routes = dict(routes or {})
+        self.ready = lambda: True
         self.tracer = tracing.PhaseTimer()
         outer = self
 
@@ -75,8 +76,15 @@ class ExtenderServer:
 
             def do_GET(self):
                 p = self.path.split("?")[0]
-                if p in ("/healthz", "/health", "/readyz"):
+                if p in ("/healthz", "/health"):
                     return self._send(200, b"ok", "text/plain")
+                if p == "/readyz":
+                    # Only the lease holder is Ready, so the Service routes
+                    # extender verbs and agent pushes to the one replica whose
+                    # ledger is authoritative.
+                    if outer.ready():
+                        return self._send(200, b"ok", "text/plain")
+                    return self._send(503, b"standby", "text/plain")
                 if p == "/metrics":
                     return self._send(200, outer.platform.expose_metrics().encode(),
                                       "text/plain; version=0.0.4")
@@ -118,9 +126,28 @@ class ExtenderServer:
                     out = json.dumps({"error": f"{type(e).__name__}: {e}"})
                 return self._send(200, out.encode())
 
+        self._handler = H
         self.httpd = ThreadingHTTPServer((host, port), H)
         self.httpd.daemon_threads = True
         self.thread = threading.Thread(target=self.httpd.serve_forever, daemon=True)
+        self._extra: list = []
+
+    def add_tls_listener(self, host: str, port: int, certfile: str, keyfile: str):
+        """Serve the same routes over HTTPS on a second port — the apiserver only
+        calls admission webhooks over TLS, while kube-scheduler talks to the
+        extender in-cluster over plain HTTP (reference webhook settings:
+        deploy/helm/kgwe/values.yaml:375-392, service port 443)."""
+        import ssl  # noqa: PLC0415
+
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+        ctx.load_cert_chain(certfile, keyfile)
+        srv = ThreadingHTTPServer((host, port), self._handler)
+        srv.daemon_threads = True
+        srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+        t = threading.Thread(target=srv.serve_forever, daemon=True)
+        self._extra.append((srv, t))
+        return srv
 
     @property
     def url(self) -> str:
@@ -162,8 +189,13 @@ class ExtenderServer:
 
     def start(self) -> "ExtenderServer":
         self.thread.start()
+        for _, t in self._extra:
+            t.start()
         return self
 
     def stop(self) -> None:
+        for srv, _ in self._extra:
+            srv.shutdown()
+            srv.server_close()
         self.httpd.shutdown()
         self.httpd.server_close()

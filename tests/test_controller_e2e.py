@@ -184,3 +184,20 @@ def test_config_rejects_unknown_keys(tmp_path):
     f.write_text("bogus: 1\n")
     with pytest.raises(ConfigError):
         load_config(DEFAULTS, str(f))
+
+
+def test_leader_election_single_holder_and_failover():
+    from kgwe.controller.leader import LeaderElector
+
+    api = FakeApiServer().start()
+    try:
+        a = LeaderElector(KubeClient(api.url), "kgwe-controller", "a", lease_s=1.0)
+        b = LeaderElector(KubeClient(api.url), "kgwe-controller", "b", lease_s=1.0)
+        t0 = time.time()
+        assert a.try_acquire_or_renew(t0)
+        assert not b.try_acquire_or_renew(t0 + 0.1)
+        assert a.try_acquire_or_renew(t0 + 0.5)      # renew
+        assert b.try_acquire_or_renew(t0 + 3.0)      # a's lease expired -> failover
+        assert not a.try_acquire_or_renew(t0 + 3.1)
+    finally:
+        api.stop()
