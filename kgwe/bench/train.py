@@ -56,12 +56,17 @@ class Trainer:
             shard_model(self.model)
             log(info, f"FSDP2 sharded over {info.world_size} rank(s)")
         self.opt = FusedAdamW(self.model.parameters(), lr=tc.lr)
-        g = torch.Generator(device=dev).manual_seed(tc.seed + info.rank)
-        self.tokens = torch.randint(0, self.cfg.vocab_size, (tc.micro_batch, tc.seq_len + 1),
-                                    device=dev, generator=g)
+        self._gen = torch.Generator(device=dev).manual_seed(tc.seed + info.rank)
+        self.tokens = torch.empty((tc.micro_batch, tc.seq_len + 1), dtype=torch.long, device=dev)
         self.last_loss: torch.Tensor | None = None
 
+    def next_batch(self) -> None:
+        """A fresh uniform-random batch every step (generated on device, ~10 us),
+        so the loss stays near ln(vocab) instead of memorising one batch."""
+        self.tokens.random_(0, self.cfg.vocab_size, generator=self._gen)
+
     def step(self) -> torch.Tensor:
+        self.next_batch()
         inp = self.tokens[:, :-1]
         lab = self.tokens[:, 1:]
         loss = self.model(inp, lab)

@@ -20,6 +20,7 @@ from ..core import Platform, make_fixture
 from ..extender.server import ExtenderServer
 from ..utils.config import load_config
 from .kube import KubeClient
+from .labels import NodeLabeler
 from .reconciler import Reconciler
 
 DEFAULTS = {
@@ -35,6 +36,7 @@ DEFAULTS = {
     "enforceBudgets": True,
     "optimizer": {"target": ""},
     "fakeNodes": 0,
+    "labelNodes": True,
     "tickSeconds": 5.0,
     "leaderElection": {"enabled": True, "namespace": "kube-system", "leaseName": "kgwe-controller",
                        "identity": "", "leaseSeconds": 15.0, "renewSeconds": 10.0, "retrySeconds": 2.0},
@@ -52,11 +54,18 @@ def build(cfg: dict):
     elif cfg["kube"]["url"]:
         kube = KubeClient(cfg["kube"]["url"], insecure=cfg["kube"]["insecure"])
 
+    labeler = NodeLabeler(kube) if kube is not None and cfg["labelNodes"] else None
+
     def agent_push(path, body):
         node = json.loads(body)
         name = path.rstrip("/").split("/")[-2]  # /v1/nodes/<name>/topology
         node["name"] = name
         plat.upsert_node(node)
+        if labeler is not None:
+            try:
+                labeler.update(name, node)
+            except Exception as e:  # noqa: BLE001 - labels are advisory; keep the topology
+                return 200, json.dumps({"ok": True, "labelError": str(e)}).encode()
         return 200, b'{"ok":true}'
 
     def admission(path, body):

@@ -149,6 +149,42 @@ def test_agent_push_endpoint(cluster):
     assert plat.node("pushed")["name"] == "pushed"
 
 
+def test_agent_push_labels_node(cluster):
+    """D15: node labels follow the pushed topology (link down -> island not
+    fully connected); an unchanged push does not re-patch."""
+    import http.client
+    api, kube, plat, ext, rec = cluster
+    node = plat.node("mi355x-0")
+    h, p = ext.httpd.server_address[:2]
+
+    def push(n):
+        c = http.client.HTTPConnection(h, p)
+        c.request("POST", "/v1/nodes/mi355x-0/topology", body=json.dumps(n))
+        r = c.getresponse()
+        assert r.status == 200 and "labelError" not in json.loads(r.read())
+
+    push(node)
+    labels = kube.get_node("mi355x-0")["metadata"]["labels"]
+    assert labels["kgwe.amd.com/gpu.count"] == "8"
+    assert labels["kgwe.amd.com/xgmi.fully-connected"] == "true"
+    assert labels["kgwe.amd.com/partition.compute"] == "SPX"
+    rv = kube.get_node("mi355x-0")["metadata"]["resourceVersion"]
+    push(node)
+    assert kube.get_node("mi355x-0")["metadata"]["resourceVersion"] == rv
+    g0 = node["gpus"][0]
+    peer = g0["links"][0]["peer"]
+    g0["links"][0]["up"] = False
+    for g in node["gpus"]:
+        if g["uuid"] == peer:
+            for link in g["links"]:
+                if link["peer"] == g0["uuid"]:
+                    link["up"] = False
+    push(node)
+    labels = kube.get_node("mi355x-0")["metadata"]["labels"]
+    assert labels["kgwe.amd.com/xgmi.fully-connected"] == "false"
+    assert labels["kgwe.amd.com/xgmi.links-down"] == "1"
+
+
 def test_webhook_mutates_and_validates():
     obj = gw("w", count=2, gpuRequirements={"count": 0, "mig": {"profile": "1g.10gb", "count": 2}})
     ar = {"request": {"uid": "u1", "operation": "CREATE", "object": obj}}
