@@ -18,8 +18,12 @@ What is measured
    barrier + synchronize; the max wall time over ranks is used.  Each rank
    samples amd-smi gfx_activity for its GPU during the timed steps; ``value``
    is the mean over ranks (whole-job average GPU utilisation, %).
-Synthetic tokens, random-init weights of the Llama-3-8B architecture, bf16
-compute, fp32 master weights + AdamW step inside every timed step.
+Synthetic tokens (a fresh uniform batch every step), random-init weights of
+the Llama-3-8B architecture, bf16 compute, fp32 master weights + AdamW step
+inside every timed step.  Data parallelism is sharded (ZeRO-2 family: the fp32
+master weights, Adam moments and reduced gradients are sharded over ranks;
+the 16 GB of bf16 weights stay replicated because 288 GB of HBM3E has room) —
+``--parallel fsdp`` runs PyTorch FSDP2 instead for comparison.
 """
 from __future__ import annotations
 
@@ -48,6 +52,9 @@ def parse(argv=None):
                     help="workloads pushed through the extender for the latency p99")
     ap.add_argument("--no-sched", action="store_true")
     ap.add_argument("--sdpa", action="store_true", help="force PyTorch SDPA attention")
+    ap.add_argument("--parallel", default="zero", choices=["zero", "fsdp"],
+                    help="zero: replicated bf16 weights + sharded fp32 optimizer/gradients "
+                         "(kgwe.parallel.zero, default); fsdp: PyTorch FSDP2")
     return ap.parse_args(argv)
 
 
@@ -91,7 +98,7 @@ def main(argv=None) -> int:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
     tc = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
-                     activation_checkpointing=args.ckpt)
+                     activation_checkpointing=args.ckpt, parallel=args.parallel)
     tr = Trainer(tc, info)
     res = timed_run(tr, args.steps, args.warmup)
 
@@ -121,7 +128,7 @@ def main(argv=None) -> int:
             "dtype": "bf16",
             "data": "synthetic tokens, random-init weights",
             "config": {"model": args.model, "global_batch": args.micro_batch * world,
-                       "seq_len": args.seq_len, "parallelism": f"fsdp{world}",
+                       "seq_len": args.seq_len, "parallelism": tr.parallelism,
                        "micro_batch_per_gpu": args.micro_batch,
                        "activation_checkpointing": args.ckpt},
             "p99_sched_latency_ms": round(p99, 3) if p99 is not None else None,

@@ -1,8 +1,8 @@
-"""FSDP Llama training harness (the workload the scheduler places).
+"""Data-parallel Llama training harness (the workload the scheduler places).
 
-One process per GPU (torchrun / the pod env the platform injects), FSDP2 over
-RCCL, bf16 compute, fp32 master weights, fused HIP AdamW, synthetic tokens,
-random-init weights.  Used by ``bench.py`` (timed steps + gfx_activity
+One process per GPU (torchrun / the pod env the platform injects), sharded
+data parallelism over RCCL (kgwe.parallel.zero, or FSDP2), bf16 compute, fp32
+master weights, fused HIP AdamW, synthetic tokens, random-init weights.  Used by ``bench.py`` (timed steps + gfx_activity
 sampling) and by ``__graft_entry__.smoke``.
 """
 from __future__ import annotations
@@ -18,6 +18,7 @@ from ..models import llama
 from ..ops import FusedAdamW
 from ..parallel import dist as kdist
 from ..parallel.fsdp import shard_model
+from ..parallel.zero import ShardedDataParallel
 from ..utils.amdsmi_util import UtilSampler
 
 
@@ -28,7 +29,12 @@ class TrainConfig:
     micro_batch: int = 2
     lr: float = 3e-4
     activation_checkpointing: bool = False
-    fsdp: bool = True
+    # "zero": replicated bf16 weights + sharded fp32 optimizer state with
+    #         bucketed RCCL reduce-scatter/all-gather (kgwe.parallel.zero);
+    # "fsdp": PyTorch FSDP2 (ZeRO-3 style per-block all-gathers);
+    # "none": single process, no process group.
+    parallel: str = "zero"
+    data: str = "random"  # "random": fresh uniform tokens each step; "fixed": one batch
     seed: int = 1234
 
 
@@ -50,20 +56,38 @@ class Trainer:
         log(info, f"building {tc.model} ({self.cfg.num_params() / 1e9:.2f}B params) on {dev}")
         self.model = llama.build(self.cfg, device=dev, dtype=torch.float32)
         self.model.activation_checkpointing = tc.activation_checkpointing
-        if tc.fsdp:
+        self.opt = None
+        self.dp = None
+        if tc.parallel == "fsdp":
             if not torch.distributed.is_initialized():
                 raise RuntimeError("FSDP needs a process group: kdist.init(force_group=True)")
             shard_model(self.model)
+            self.opt = FusedAdamW(self.model.parameters(), lr=tc.lr)
             log(info, f"FSDP2 sharded over {info.world_size} rank(s)")
-        self.opt = FusedAdamW(self.model.parameters(), lr=tc.lr)
+        elif tc.parallel in ("zero", "none"):
+            if tc.parallel == "none" and info.world_size > 1:
+                raise RuntimeError("parallel='none' with WORLD_SIZE > 1")
+            self.dp = ShardedDataParallel(self.model, lr=tc.lr)
+            log(info, f"sharded DP over {info.world_size} rank(s): {len(self.dp.buckets)} buckets, "
+                      f"replicated bf16 weights, fp32 optimizer shard "
+                      f"{sum(b.shard for b in self.dp.buckets) * 12 / 2**30:.1f} GiB/rank")
+        else:
+            raise ValueError(f"unknown parallel mode {tc.parallel!r}")
         self._gen = torch.Generator(device=dev).manual_seed(tc.seed + info.rank)
         self.tokens = torch.empty((tc.micro_batch, tc.seq_len + 1), dtype=torch.long, device=dev)
+        self.tokens.random_(0, self.cfg.vocab_size, generator=self._gen)
         self.last_loss: torch.Tensor | None = None
+
+    @property
+    def parallelism(self) -> str:
+        w = self.info.world_size
+        return {"fsdp": f"fsdp{w}", "zero": f"zero2-dp{w}", "none": "single"}[self.tc.parallel]
 
     def next_batch(self) -> None:
         """A fresh uniform-random batch every step (generated on device, ~10 us),
         so the loss stays near ln(vocab) instead of memorising one batch."""
-        self.tokens.random_(0, self.cfg.vocab_size, generator=self._gen)
+        if self.tc.data == "random":
+            self.tokens.random_(0, self.cfg.vocab_size, generator=self._gen)
 
     def step(self) -> torch.Tensor:
         self.next_batch()
@@ -71,8 +95,11 @@ class Trainer:
         lab = self.tokens[:, 1:]
         loss = self.model(inp, lab)
         loss.backward()
-        self.opt.step()
-        self.opt.zero_grad(set_to_none=True)
+        if self.dp is not None:
+            self.dp.step()
+        else:
+            self.opt.step()
+            self.opt.zero_grad(set_to_none=True)
         self.last_loss = loss.detach()
         return self.last_loss
 

@@ -1,9 +1,16 @@
-"""Single-launch multi-tensor AdamW over fp32 (FSDP-sharded) parameters.
+"""Single-launch multi-tensor AdamW with fp32 master weights.
 
-Works on plain tensors and on FSDP2 DTensor parameters (updates the local
-shard in place).  On a GPU the ``kgwe_adamw_step`` HIP kernel does the whole
-update in one launch; the pointer/chunk tables are rebuilt only when the
-gradient storage moves.  On CPU the fp32 reference is used.
+* fp32 parameters (incl. FSDP2 DTensor shards): updated in place.
+* bf16 parameters: the optimizer keeps an fp32 master copy (plus fp32 m, v)
+  and the kernel writes the rounded result straight back into the bf16
+  parameter — the weight the next forward reads — and reads the bf16 gradient
+  autograd produced without an up-cast pass.  This is the single-GPU /
+  replicated-weights mixed-precision path (288 GB of HBM holds bf16 weights,
+  fp32 master and both moments of an 8B model with room for activations).
+
+On a GPU the ``kgwe_adamw_step`` HIP kernel does every tensor in one launch;
+the pointer/chunk tables (``AdamPlan``) are rebuilt only when some storage
+moves.  On CPU the fp32 reference is used.
 """
 from __future__ import annotations
 
@@ -14,7 +21,7 @@ from . import reference as ref
 from ._lib import check, lib, stream
 
 _TENSOR_DT = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"),
-                       ("shadow", "<u8"), ("n", "<i8")])
+                       ("shadow", "<u8"), ("n", "<i8"), ("g_bf16", "<i4"), ("pad", "<i4")])
 _CHUNK_DT = np.dtype([("tensor", "<i4"), ("pad", "<i4"), ("start", "<i8")])
 
 
@@ -22,81 +29,112 @@ def _local(t: torch.Tensor) -> torch.Tensor:
     return t.to_local() if hasattr(t, "to_local") else t
 
 
+class AdamPlan:
+    """Pointer + chunk tables for one multi-tensor AdamW launch.
+
+    ``entries`` = [(p fp32, g fp32|bf16, m fp32, v fp32, shadow bf16|None)], all
+    contiguous with equal element counts (checked on the host: the kernel
+    trusts the table)."""
+
+    def __init__(self):
+        self._key = None
+        self._dev = None
+
+    @staticmethod
+    def _check(i, p, g, m, v, sh):
+        ok = (p.dtype == m.dtype == v.dtype == torch.float32
+              and g.dtype in (torch.float32, torch.bfloat16)
+              and all(t.is_contiguous() for t in (p, g, m, v))
+              and p.numel() == g.numel() == m.numel() == v.numel()
+              and (sh is None or (sh.dtype == torch.bfloat16 and sh.is_contiguous()
+                                  and sh.numel() == p.numel())))
+        if not ok:
+            raise ValueError(f"AdamW: entry {i} violates the kernel contract "
+                             f"(p {p.dtype}/{tuple(p.shape)}, g {g.dtype}/{tuple(g.shape)}, "
+                             f"shadow {None if sh is None else (sh.dtype, tuple(sh.shape))})")
+
+    def _tables(self, entries):
+        key = tuple((p.data_ptr(), g.data_ptr(), g.dtype == torch.bfloat16) for p, g, *_ in entries)
+        if key == self._key:
+            return self._dev
+        L = lib()
+        chunk = L.kgwe_adamw_chunk_elems()
+        assert L.kgwe_adamw_tensor_bytes() == _TENSOR_DT.itemsize
+        tens = np.zeros(len(entries), dtype=_TENSOR_DT)
+        chunks = []
+        for i, (p, g, m, v, sh) in enumerate(entries):
+            self._check(i, p, g, m, v, sh)
+            tens[i] = (p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                       0 if sh is None else sh.data_ptr(), p.numel(),
+                       int(g.dtype == torch.bfloat16), 0)
+            chunks.extend((i, 0, s) for s in range(0, p.numel(), chunk))
+        ch = np.array(chunks, dtype=_CHUNK_DT)
+        dev = entries[0][0].device
+        # Pinned staging + async H2D on the compute stream: no host sync.  The
+        # staging buffers stay referenced until the next rebuild, long after
+        # the stream consumed them.
+        t_host = torch.from_numpy(tens.view(np.uint8).copy()).pin_memory()
+        c_host = torch.from_numpy(ch.view(np.uint8).copy()).pin_memory()
+        self._dev = (t_host.to(dev, non_blocking=True), c_host.to(dev, non_blocking=True),
+                     len(chunks), t_host, c_host)
+        self._key = key
+        return self._dev
+
+    def launch(self, entries, lr, b1, b2, eps, wd, step, grad_scale=1.0):
+        if not entries:
+            return
+        p0 = entries[0][0]
+        if p0.is_cuda:
+            t_dev, c_dev, n = self._tables(entries)[:3]
+            check(lib().kgwe_adamw_step(t_dev.data_ptr(), c_dev.data_ptr(), n, lr, b1, b2, eps, wd,
+                                        step, grad_scale, stream(p0)), "adamw_step")
+            return
+        for p, g, m, v, sh in entries:
+            gg = g.float() * grad_scale if grad_scale != 1.0 else g.float()
+            ref.adamw_(p, gg, m, v, lr, b1, b2, eps, wd, step)
+            if sh is not None:
+                sh.copy_(p)
+
+
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._step = 0
-        self._tables: dict = {}
+        self._plans: dict[int, AdamPlan] = {}
 
-    def _group_tensors(self, group):
-        ps, gs, ms, vs = [], [], [], []
+    def _entries(self, group):
+        out = []
         for p in group["params"]:
             if p.grad is None:
                 continue
             st = self.state[p]
             lp = _local(p).detach() if hasattr(p, "to_local") else p.data
-            if "exp_avg" not in st:
-                st["exp_avg"] = torch.zeros_like(lp, dtype=torch.float32)
-                st["exp_avg_sq"] = torch.zeros_like(lp, dtype=torch.float32)
-            g = _local(p.grad)
             if lp.numel() == 0:
                 continue
-            ps.append(lp)
-            gs.append(g if g.dtype == torch.float32 else g.float())
-            ms.append(st["exp_avg"])
-            vs.append(st["exp_avg_sq"])
-        return ps, gs, ms, vs
-
-    def _device_tables(self, gi, ps, gs, ms, vs):
-        key = tuple(t.data_ptr() for t in gs) + tuple(t.data_ptr() for t in ps)
-        cached = self._tables.get(gi)
-        if cached is not None and cached[0] == key:
-            return cached[1], cached[2], cached[3]
-        L = lib()
-        chunk = L.kgwe_adamw_chunk_elems()
-        tens = np.zeros(len(ps), dtype=_TENSOR_DT)
-        chunks = []
-        for i, (p, g, m, v) in enumerate(zip(ps, gs, ms, vs)):
-            # Kernel contract: fp32, contiguous, equal element counts.
-            if not (p.dtype == g.dtype == m.dtype == v.dtype == torch.float32
-                    and p.is_contiguous() and g.is_contiguous()
-                    and p.numel() == g.numel() == m.numel() == v.numel()):
-                raise ValueError(f"FusedAdamW: tensor {i} violates the kernel contract "
-                                 f"(p {p.dtype}/{p.shape}, g {g.dtype}/{g.shape})")
-            tens[i] = (p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), 0, p.numel())
-            for s in range(0, p.numel(), chunk):
-                chunks.append((i, 0, s))
-        ch = np.array(chunks, dtype=_CHUNK_DT)
-        dev = ps[0].device
-        # Pinned staging + async H2D on the compute stream: no host sync.  The
-        # staging buffers stay referenced by the cache entry until the next
-        # rebuild of this group, after which the stream has long consumed them.
-        t_host = torch.from_numpy(tens.view(np.uint8).copy())
-        c_host = torch.from_numpy(ch.view(np.uint8).copy())
-        if dev.type == "cuda":
-            t_host, c_host = t_host.pin_memory(), c_host.pin_memory()
-        t_dev = t_host.to(dev, non_blocking=True)
-        c_dev = c_host.to(dev, non_blocking=True)
-        self._tables[gi] = (key, t_dev, c_dev, len(chunks), t_host, c_host)
-        return t_dev, c_dev, len(chunks)
+            g = _local(p.grad)
+            if lp.dtype == torch.bfloat16:
+                if "master" not in st:
+                    st["master"] = lp.float()
+                master, shadow = st["master"], lp
+            elif lp.dtype == torch.float32:
+                master, shadow = lp, None
+                if g.dtype not in (torch.float32, torch.bfloat16):
+                    g = g.float()
+            else:
+                raise ValueError(f"FusedAdamW: unsupported parameter dtype {lp.dtype}")
+            if "exp_avg" not in st:
+                st["exp_avg"] = torch.zeros_like(master)
+                st["exp_avg_sq"] = torch.zeros_like(master)
+            out.append((master, g.contiguous(), st["exp_avg"], st["exp_avg_sq"], shadow))
+        return out
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         self._step += 1
         for gi, group in enumerate(self.param_groups):
-            ps, gs, ms, vs = self._group_tensors(group)
-            if not ps:
-                continue
+            entries = self._entries(group)
             b1, b2 = group["betas"]
-            if ps[0].is_cuda:
-                t_dev, c_dev, n = self._device_tables(gi, ps, gs, ms, vs)
-                check(lib().kgwe_adamw_step(t_dev.data_ptr(), c_dev.data_ptr(), n,
-                                            group["lr"], b1, b2, group["eps"],
-                                            group["weight_decay"], self._step, 1.0,
-                                            stream(ps[0])), "adamw_step")
-            else:
-                for p, g, m, v in zip(ps, gs, ms, vs):
-                    ref.adamw_(p, g, m, v, group["lr"], b1, b2, group["eps"],
-                               group["weight_decay"], self._step)
+            self._plans.setdefault(gi, AdamPlan()).launch(
+                entries, group["lr"], b1, b2, group["eps"], group["weight_decay"], self._step)
         return loss

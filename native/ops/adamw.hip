@@ -1,11 +1,15 @@
-// Multi-tensor fused AdamW for fp32 master parameters (FSDP shards).
+// Multi-tensor fused AdamW for fp32 master parameters.
 //
-// One launch updates every parameter shard: the host builds a chunk table
-// (tensor index, element offset) once, the per-tensor pointer table is a
-// small device array refreshed when gradient storage moves.  Each lane
-// streams 4 fp32 (16 B) of p, g, m, v per step and writes back p, m, v (and
-// optionally a bf16 shadow copy of p), i.e. 28 B/param — HBM-bound, so the
-// only goal is full-width coalesced access and a single launch.
+// One launch updates every parameter (or every optimizer-state shard): the
+// host builds a chunk table (tensor index, element offset) once, the
+// per-tensor pointer table is a small device array refreshed only when
+// gradient storage moves.  Each lane streams 4 elements (16 B fp32 of p, m, v;
+// 16 B fp32 or 8 B bf16 of g) and writes back p, m, v plus an optional bf16
+// copy of p — the live bf16 model weight the next forward reads.  That copy is
+// what removes the separate cast/all-gather-copy pass of a master-weight
+// scheme, and reading bf16 gradients straight from autograd's output removes
+// the fp32 up-cast pass.  HBM-bound (26-30 B/param), so the only goals are
+// full-width coalesced access and a single launch.
 //
 //   m = b1 m + (1-b1) g ;  v = b2 v + (1-b2) g^2
 //   p = p - lr * (m / bc1 / (sqrt(v / bc2) + eps) + wd * p)
@@ -15,11 +19,13 @@ using namespace kgwe;
 
 struct AdamTensor {
   float* p;
-  const float* g;
+  const void* g;   // fp32 or bf16 (g_bf16)
   float* m;
   float* v;
   bf16_t* shadow;  // optional bf16 copy of p (nullptr = none)
   int64_t n;
+  int32_t g_bf16;
+  int32_t pad;
 };
 
 struct AdamChunk {
@@ -32,49 +38,81 @@ constexpr int kChunk = 256 * 4 * 16;  // elements per workgroup task (64 KiB fp3
 
 namespace {
 
+struct AdamArgs {
+  float lr, b1, b2, eps, wd, bc1, bc2_sqrt_inv, grad_scale;
+};
+
+__device__ __forceinline__ float adam_one(float& p, float& m, float& v, float g, const AdamArgs& a) {
+  const float gj = g * a.grad_scale;
+  m = a.b1 * m + (1.f - a.b1) * gj;
+  v = a.b2 * v + (1.f - a.b2) * gj * gj;
+  const float denom = sqrtf(v) * a.bc2_sqrt_inv + a.eps;
+  p -= a.lr * (m / a.bc1 / denom + a.wd * p);
+  return p;
+}
+
+template <bool GB>
+__device__ __forceinline__ void adam_range(const AdamTensor& t, int64_t start, int64_t end,
+                                           const AdamArgs& a) {
+  const float* gf = static_cast<const float*>(t.g);
+  const bf16_t* gb = static_cast<const bf16_t*>(t.g);
+  for (int64_t i = start + threadIdx.x * 4; i < end; i += 256 * 4) {
+    const bool aligned =
+        ((reinterpret_cast<uintptr_t>(t.p + i) | reinterpret_cast<uintptr_t>(t.m + i) |
+          reinterpret_cast<uintptr_t>(t.v + i)) & 15) == 0 &&
+        (GB ? (reinterpret_cast<uintptr_t>(gb + i) & 7) == 0
+            : (reinterpret_cast<uintptr_t>(gf + i) & 15) == 0) &&
+        (t.shadow == nullptr || (reinterpret_cast<uintptr_t>(t.shadow + i) & 7) == 0);
+    if (i + 4 <= end && aligned) {
+      f32x4 p = *reinterpret_cast<const f32x4*>(t.p + i);
+      f32x4 m = *reinterpret_cast<const f32x4*>(t.m + i);
+      f32x4 v = *reinterpret_cast<const f32x4*>(t.v + i);
+      float g[4];
+      if constexpr (GB) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(gb + i);
+        g[0] = __uint_as_float(raw.x << 16);
+        g[1] = __uint_as_float(raw.x & 0xffff0000u);
+        g[2] = __uint_as_float(raw.y << 16);
+        g[3] = __uint_as_float(raw.y & 0xffff0000u);
+      } else {
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(gf + i);
+        g[0] = gv[0]; g[1] = gv[1]; g[2] = gv[2]; g[3] = gv[3];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pj = p[j], mj = m[j], vj = v[j];
+        adam_one(pj, mj, vj, g[j], a);
+        p[j] = pj; m[j] = mj; v[j] = vj;
+      }
+      *reinterpret_cast<f32x4*>(t.p + i) = p;
+      *reinterpret_cast<f32x4*>(t.m + i) = m;
+      *reinterpret_cast<f32x4*>(t.v + i) = v;
+      if (t.shadow) {
+        uint2 o;
+        o.x = static_cast<unsigned>(f2bf(p[0])) | (static_cast<unsigned>(f2bf(p[1])) << 16);
+        o.y = static_cast<unsigned>(f2bf(p[2])) | (static_cast<unsigned>(f2bf(p[3])) << 16);
+        *reinterpret_cast<uint2*>(t.shadow + i) = o;
+      }
+    } else {
+      for (int64_t k = i; k < end && k < i + 4; ++k) {
+        float pk = t.p[k], mk = t.m[k], vk = t.v[k];
+        adam_one(pk, mk, vk, GB ? bf2f(gb[k]) : gf[k], a);
+        t.p[k] = pk; t.m[k] = mk; t.v[k] = vk;
+        if (t.shadow) t.shadow[k] = f2bf(pk);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(
     const AdamTensor* __restrict__ tensors, const AdamChunk* __restrict__ chunks,
-    int nchunks, float lr, float b1, float b2, float eps, float wd, float bc1,
-    float bc2_sqrt_inv, float grad_scale) {
+    int nchunks, AdamArgs a) {
   for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
     const AdamChunk ch = chunks[ci];
     const AdamTensor t = tensors[ch.tensor];
     const int64_t end = (ch.start + kChunk < t.n) ? ch.start + kChunk : t.n;
-    for (int64_t i = ch.start + threadIdx.x * 4; i < end; i += 256 * 4) {
-      if (i + 4 <= end && ((reinterpret_cast<uintptr_t>(t.p + i) & 15) == 0) &&
-          ((reinterpret_cast<uintptr_t>(t.g + i) & 15) == 0)) {
-        f32x4 p = *reinterpret_cast<const f32x4*>(t.p + i);
-        const f32x4 g = *reinterpret_cast<const f32x4*>(t.g + i);
-        f32x4 m = *reinterpret_cast<const f32x4*>(t.m + i);
-        f32x4 v = *reinterpret_cast<const f32x4*>(t.v + i);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float gj = g[j] * grad_scale;
-          m[j] = b1 * m[j] + (1.f - b1) * gj;
-          v[j] = b2 * v[j] + (1.f - b2) * gj * gj;
-          const float denom = sqrtf(v[j]) * bc2_sqrt_inv + eps;
-          p[j] -= lr * (m[j] / bc1 / denom + wd * p[j]);
-        }
-        *reinterpret_cast<f32x4*>(t.p + i) = p;
-        *reinterpret_cast<f32x4*>(t.m + i) = m;
-        *reinterpret_cast<f32x4*>(t.v + i) = v;
-        if (t.shadow) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) t.shadow[i + j] = f2bf(p[j]);
-        }
-      } else {
-        for (int64_t k = i; k < end && k < i + 4; ++k) {
-          const float gj = t.g[k] * grad_scale;
-          const float mk = b1 * t.m[k] + (1.f - b1) * gj;
-          const float vk = b2 * t.v[k] + (1.f - b2) * gj * gj;
-          t.m[k] = mk;
-          t.v[k] = vk;
-          const float pk = t.p[k] - lr * (mk / bc1 / (sqrtf(vk) * bc2_sqrt_inv + eps) + wd * t.p[k]);
-          t.p[k] = pk;
-          if (t.shadow) t.shadow[k] = f2bf(pk);
-        }
-      }
-    }
+    if (t.g_bf16) adam_range<true>(t, ch.start, end, a);
+    else adam_range<false>(t, ch.start, end, a);
   }
 }
 
@@ -90,12 +128,14 @@ KGWE_API int kgwe_adamw_step(const void* tensors, const void* chunks, int nchunk
                              float lr, float b1, float b2, float eps, float wd,
                              int step, float grad_scale, hipStream_t s) {
   if (nchunks <= 0) return 0;
-  const float bc1 = 1.f - powf(b1, static_cast<float>(step));
-  const float bc2 = 1.f - powf(b2, static_cast<float>(step));
+  AdamArgs a;
+  a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
+  a.bc1 = 1.f - powf(b1, static_cast<float>(step));
+  a.bc2_sqrt_inv = 1.f / sqrtf(1.f - powf(b2, static_cast<float>(step)));
+  a.grad_scale = grad_scale;
   const int grid = nchunks < 4096 ? nchunks : 4096;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, s,
                      static_cast<const AdamTensor*>(tensors),
-                     static_cast<const AdamChunk*>(chunks), nchunks, lr, b1, b2, eps,
-                     wd, bc1, 1.f / sqrtf(bc2), grad_scale);
+                     static_cast<const AdamChunk*>(chunks), nchunks, a);
   return KGWE_CHECK_LAUNCH();
 }

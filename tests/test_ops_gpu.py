@@ -3,6 +3,7 @@
 All tests here run on a real MI355X (``pytest -m gpu`` via gpurun) and exercise
 the HIP path only: the library must be loaded (no silent fallback).
 """
+import numpy as np
 import pytest
 import torch
 
@@ -135,6 +136,38 @@ def test_fused_adamw_matches_reference():
         assert torch.allclose(p.detach(), r, rtol=1e-5, atol=1e-6)
 
 
+def test_fused_adamw_bf16_master_weights():
+    """bf16 params: fp32 master kept by the optimizer, bf16 grads read directly,
+    rounded result written back into the bf16 parameter (odd sizes and an
+    unaligned view exercise the scalar tail path)."""
+    from kgwe.ops import FusedAdamW
+
+    torch.manual_seed(6)
+    shapes = [(1000,), (333, 77), (4096, 17), (5,)]
+    base = torch.randn(sum(int(np.prod(s)) for s in shapes) + 3, device=DEV)
+    ps, off = [], 3  # offset 3 elements: 6-byte misaligned bf16 storage
+    flat = base.to(torch.bfloat16)
+    for s in shapes:
+        n = int(np.prod(s))
+        ps.append(torch.nn.Parameter(flat[off:off + n].view(s)))
+        off += n
+    master = [p.detach().float().clone() for p in ps]
+    ms = [torch.zeros_like(p) for p in master]
+    vs = [torch.zeros_like(p) for p in master]
+    opt = FusedAdamW(ps, lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        gs = [torch.randn(p.shape, device=DEV).to(torch.bfloat16) for p in ps]
+        for p, g in zip(ps, gs):
+            p.grad = g.clone()
+        opt.step()
+        for p, g, m, v in zip(master, gs, ms, vs):
+            ref.adamw_(p, g.float(), m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, step)
+    for p, r in zip(ps, master):
+        assert p.dtype == torch.bfloat16
+        assert torch.allclose(opt.state[p]["master"], r, rtol=1e-5, atol=1e-6)
+        assert torch.equal(p.detach(), r.to(torch.bfloat16))
+
+
 def test_llama_tiny_train_step_hip():
     """End-to-end forward/backward/optimizer of the tiny Llama on the HIP path,
     checked against the same model on the fp32 CPU reference path."""
@@ -165,9 +198,10 @@ def test_rope_rejects_out_of_contract_tables():
         K.rope_qkv(qkv, cos[:10], sin[:10], 64, 4, 2, 128)
 
 
-def test_fsdp2_single_rank_train_step():
-    """The exact path bench.py runs: FSDP2 (1 rank, RCCL) + bf16 mixed precision
-    + HIP ops + fused AdamW."""
+@pytest.mark.parametrize("parallel", ["zero", "fsdp"])
+def test_single_rank_train_step(parallel):
+    """The exact paths bench.py runs (1 rank, RCCL process group): sharded DP
+    (default) and FSDP2, bf16 mixed precision + HIP ops + fused AdamW."""
     import torch.distributed as dist
 
     from kgwe.bench.train import TrainConfig, Trainer
@@ -175,7 +209,8 @@ def test_fsdp2_single_rank_train_step():
 
     info = kd.init(force_group=True)
     try:
-        tr = Trainer(TrainConfig(model="tiny", seq_len=256, micro_batch=2), info)
+        tr = Trainer(TrainConfig(model="tiny", seq_len=256, micro_batch=2, parallel=parallel,
+                                 data="fixed"), info)
         losses = [tr.step().item() for _ in range(3)]
         assert all(torch.isfinite(torch.tensor(losses)))
         assert losses[-1] < losses[0]
