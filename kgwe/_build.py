@@ -111,10 +111,17 @@ def build_core(force: bool = False, jobs: int = 8) -> Path | None:
     incs = [core_dir, Path(pybind11.get_include()), Path(sysconfig.get_paths()["include"]),
             Path("/opt/rocm/include")]
     cxx = os.environ.get("CXX", "g++")
+    flags, link = list(CXX_FLAGS), ["-ldl", "-lpthread"]
+    if os.environ.get("KGWE_CORE_SANITIZE") == "1":
+        # Host-only ASan + UBSan build of the platform core (the
+        # reference's `go test -race`); load with LD_PRELOAD=libasan.so.
+        san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        flags += san
+        link += san
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, cxx, CXX_FLAGS, incs, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, cxx, flags, incs, force), srcs))
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return _link(objs, LIB / f"_kgwe_core{suffix}", cxx, ["-ldl", "-lpthread"], force)
+    return _link(objs, LIB / f"_kgwe_core{suffix}", cxx, link, force)
 
 
 def build_all(force: bool = False, jobs: int = 8) -> list[Path]:

@@ -236,7 +236,8 @@ PYBIND11_MODULE(_kgwe_core, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("schedule_gang", [](PyPlatform& s, const std::string& arr) {
         std::vector<WorkloadRequest> ws;
-        for (const auto& j : Json::parse(arr).items()) ws.push_back(workload_from_json(j));
+        const Json parsed = Json::parse(arr);  // keep alive: items() is a reference into it
+        for (const auto& j : parsed.items()) ws.push_back(workload_from_json(j));
         return list_json(s.p->scheduler()->schedule_gang(ws));
       }, py::call_guard<py::gil_scoped_release>())
       .def("release", [](PyPlatform& s, const std::string& uid, double now) { return s.p->release(uid, now); })
