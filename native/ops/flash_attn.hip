@@ -1,13 +1,15 @@
 // Causal GQA flash attention for gfx950 (MI355X), bf16 in / fp32 accumulate,
 // head_dim 128, written directly on v_mfma_f32_32x32x16_bf16.
 //
-// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head)):
+// Forward (one workgroup = 8 waves = 256 query rows of one (batch, head)):
 //   * each wave owns 32 query rows; Q stays in VGPRs for the whole pass
 //     (8 k-steps x bf16x8 = 32 VGPRs);
-//   * K/V tiles of 64 keys are staged through LDS (K row-major with a 16-B row
-//     pad: conflict-free ds_read_b128; V transposed with an 8-B pad:
-//     conflict-free ds_read_b64), register-prefetched one tile ahead so the
-//     global loads of tile t+1 overlap the MFMAs of tile t;
+//   * K/V tiles of 64 keys are double-buffered in LDS (K row-major with a
+//     16-B row pad: conflict-free ds_read_b128; V row-major in an XOR-swizzled
+//     image read with the gfx950 hardware transpose ds_read_b64_tr_b16, so
+//     nothing is transposed on the write side); the global loads of tile t+1
+//     are issued before tile t's MFMAs and stored after them, one barrier per
+//     tile; O is rescaled only when some row's running max moved;
 //   * S^T = K Q^T is computed with the KEY on the accumulator rows and the
 //     query on the lane, so every lane owns one query row: the online-softmax
 //     row max / row sum are 32 in-lane ops + one cross-half exchange, and
@@ -24,16 +26,18 @@
 //
 // Backward (FA2 split, no dQ atomics => deterministic):
 //   * dkdv kernel: one workgroup = 4 waves = 128 keys of one (batch, kv-head);
-//     each wave owns 32 keys, keeps K and V in VGPRs and dK^T / dV^T
-//     accumulators (2 x 64 fp32) in VGPRs, and sweeps every query head of
+//     each wave owns 32 keys, keeps K and the dK^T / dV^T accumulators
+//     (2 x 64 fp32) in VGPRs (V rows come from a per-workgroup LDS image, so
+//     the kernel fits 256 VGPRs and two workgroups share a CU), and sweeps every query head of
 //     its GQA group x every 32-row query tile: S (key on the lane),
 //     P = exp2(S*c - lse2), dV^T += dO^T P, dP = dO V^T, dS = P (dP - delta),
 //     dK^T += Q^T dS — all operands of the P/dS products come from the
-//     accumulators (no LDS round trip); Q / dO tiles are staged in LDS in
-//     both row and transposed images.
+//     accumulators (no LDS round trip); Q / dO tiles are double-buffered in
+//     ONE swizzled image each, read by rows (ds_read_b128) for S and dP and
+//     by columns (ds_read_b64_tr_b16) for dV^T and dK^T.
 //   * dq kernel: one workgroup = 128 query rows of one (batch, head) (the
 //     forward's geometry, query on the lane): recomputes S^T and dP^T and
-//     accumulates dQ^T += K^T dS^T with K^T staged transposed in LDS.
+//     accumulates dQ^T += K^T dS^T, K^T read transposed from the K image.
 //   * delta = rowsum(dO * O) by a small preprocess kernel.
 #include "common.h"
 
@@ -46,10 +50,9 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
 
 constexpr int HD = 128;             // head dim
-constexpr int BQ = 128;             // query rows per forward workgroup
+constexpr int BQ = 128;             // query rows per dQ workgroup
 constexpr int BKV = 64;             // keys per forward tile
 constexpr int KST = HD + 8;         // K row stride in LDS (bf16): 272 B
-constexpr int VST = BKV + 4;        // V^T row stride in LDS (bf16): 136 B
 
 __device__ __forceinline__ mfma8 as_m(bf16x8 v) { return __builtin_bit_cast(mfma8, v); }
 
@@ -88,19 +91,45 @@ __device__ __forceinline__ void decode(int nQB, int G, int Hkv, bool causal, int
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
+// V tile image for the hardware-transposed read (ds_read_b64_tr_b16): plain
+// 256-B rows [key][d] written straight from HBM with 16-B stores, 16-B chunks
+// XOR-swizzled by row so the transposed reads of a 32-lane half (4 keys x 64 B)
+// hit 64 distinct banks (cdna_hip_programming.md T10, layout (b)).
+__device__ __forceinline__ int v_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ u16x4 tr_read(const bf16_t* lds_base, int byte_off) {
+  typedef __attribute__((ext_vector_type(4))) short s4;
+  const s4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4*)(reinterpret_cast<const char*>(lds_base) + byte_off));
+  return __builtin_bit_cast(u16x4, r);
+}
+
+constexpr int BQF = 256;            // query rows per forward workgroup (8 waves x 32)
+constexpr int KTILE = BKV * KST;    // bf16 elements of one K buffer
+constexpr int VTILE = BKV * HD;     // bf16 elements of one V buffer
+
+// One workgroup = 8 waves = 256 query rows of one (batch, head); K/V tiles of
+// 64 keys double-buffered in LDS (67 KB): the global loads of tile t+1 are
+// issued before tile t's MFMAs and written to the other buffer after them, so
+// one barrier per tile separates the phases.
+__global__ __launch_bounds__(512) void fa_fwd_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, float* __restrict__ lse2, int S, int Hq, int Hkv, float c,
     int causal, int nQB) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * KST];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[HD * VST];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * KTILE];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * VTILE];
   int b, h, hkv, qb;
   decode(nQB, Hq / Hkv, Hkv, causal, &b, &h, &hkv, &qb);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lq = lane & 31, hh = lane >> 5;
-  const int q0 = qb * BQ + w * 32;
+  const int q0 = qb * BQF + w * 32;
   const int qrow = q0 + lq;
   const size_t qs = static_cast<size_t>(Hq) * HD, kvs = static_cast<size_t>(Hkv) * HD;
+  // The second-dispatched half loses VALU arbitration on every segment;
+  // one static priority bump evens it out (MI355X_MICROARCH.md, two waves/SIMD).
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
   bf16x8 qf[8];
   {
@@ -113,94 +142,123 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   for (int i = 0; i < 4; ++i) oacc[i] = f32x16{};
   float m = -INFINITY, l = 0.f;
 
-  const int kv_end = causal ? min(S, qb * BQ + BQ) : S;
+  const int kv_end = causal ? min(S, qb * BQF + BQF) : S;
   const int ntiles = (kv_end + BKV - 1) / BKV;
   const bf16_t* kb = k + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
   const bf16_t* vb = v + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
-  bf16x8 kr[4], vr[4];
+  // Staging: thread t moves chunks (key, ch) = ((t + 512 i) >> 4, t & 15), i = 0, 1.
+  const int skey = threadIdx.x >> 4, sch = threadIdx.x & 15;
+  bf16x8 kr[2], vr[2];
   auto gload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = threadIdx.x + 256 * i, key = idx >> 4, ch = idx & 15;
-      const int s = kt * BKV + key;
+    for (int i = 0; i < 2; ++i) {
+      const int s = kt * BKV + skey + 32 * i;
       if (s < S) {
-        kr[i] = ld16(kb + static_cast<size_t>(s) * kvs + ch * 8);
-        vr[i] = ld16(vb + static_cast<size_t>(s) * kvs + ch * 8);
+        kr[i] = ld16(kb + static_cast<size_t>(s) * kvs + sch * 8);
+        vr[i] = ld16(vb + static_cast<size_t>(s) * kvs + sch * 8);
       } else {
         kr[i] = bf16x8{};
         vr[i] = bf16x8{};
       }
     }
   };
-  gload(0);
-  for (int kt = 0; kt < ntiles; ++kt) {
-    __syncthreads();  // every wave is done reading the previous tile
+  auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = threadIdx.x + 256 * i, key = idx >> 4, ch = idx & 15;
-      *reinterpret_cast<bf16x8*>(&Ks[key * KST + ch * 8]) = kr[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * VST + key] = vr[i][j];
+    for (int i = 0; i < 2; ++i) {
+      const int key = skey + 32 * i;
+      *reinterpret_cast<bf16x8*>(&Ks[buf * KTILE + key * KST + sch * 8]) = kr[i];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(&Vs[buf * VTILE]) + v_off(key, sch)) = vr[i];
     }
-    __syncthreads();
-    if (kt + 1 < ntiles) gload(kt + 1);  // in flight during this tile's MFMAs
-    const int k0 = kt * BKV;
-    if (causal && k0 > q0 + 31) continue;  // tile entirely above this wave's diagonal
+  };
+  // Transposed-read lane geometry (T10): group G = lane >> 4 reads keys
+  // base + 4*(G >> 1) + qq at d chunk 4*db + 2*(G & 1) + (pp >> 1), byte 8*(pp & 1).
+  const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
+  const int tr_row = 4 * (trG >> 1) + trq;
+  const int tr_ch = 2 * (trG & 1) + (trp >> 1);
+  const int tr_byte = 8 * (trp & 1);
 
-    f32x16 sacc[2] = {f32x16{}, f32x16{}};
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) gload(kt + 1);  // lands during this tile's MFMAs
+    const int k0 = kt * BKV;
+    if (!causal || k0 <= q0 + 31) {  // else: tile entirely above this wave's diagonal
+      const bf16_t* Kc = Ks + cur * KTILE;
+      const bf16_t* Vc = Vs + cur * VTILE;
+      f32x16 sacc[2] = {f32x16{}, f32x16{}};
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
-        sacc[st] = mfma(*reinterpret_cast<const bf16x8*>(&Ks[(st * 32 + lq) * KST + 16 * t + 8 * hh]),
-                        qf[t], sacc[st]);
-    float mx = -INFINITY;
+        for (int t = 0; t < 8; ++t)
+          sacc[st] = mfma(ld16(&Kc[(st * 32 + lq) * KST + 16 * t + 8 * hh]), qf[t], sacc[st]);
+      float mx = -INFINITY;
+      const bool edge = (causal && k0 + BKV - 1 > q0) || k0 + BKV > S;  // wave-uniform
+      if (edge) {
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+        for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + st * 32 + acc_row(r, hh);
-        float s = sacc[st][r] * c;
-        if (key >= S || (causal && key > qrow)) s = -INFINITY;
-        sacc[st][r] = s;
-        mx = fmaxf(mx, s);
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + st * 32 + acc_row(r, hh);
+            float s = sacc[st][r] * c;
+            if (key >= S || (causal && key > qrow)) s = -INFINITY;
+            sacc[st][r] = s;
+            mx = fmaxf(mx, s);
+          }
+      } else {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            sacc[st][r] *= c;
+            mx = fmaxf(mx, sacc[st][r]);
+          }
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-    const float m_new = fmaxf(m, mx);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m - m_use);
-    float rs = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+      const float m_new = fmaxf(m, mx);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      // Rescale O only when some row's max moved (exact; after the first few
+      // tiles the running max rarely changes).
+      if (__any(m_new > m)) {
+        const float alpha = exp2f(m - m_use);
+        l *= alpha;
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+        for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(sacc[st][r] - m_use);
-        sacc[st][r] = p;
-        rs += p;
+          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
       }
-    rs += __shfl_xor(rs, 32, kWave);
-    l = l * alpha + rs;
-    m = m_new;
+      m = m_new;
+      float rs = 0.f;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-    // O^T += V^T P : P (key rows, query on lane) is the B operand as is.
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(sacc[st][r] - m_use);
+          sacc[st][r] = p;
+          rs += p;
+        }
+      l += rs + __shfl_xor(rs, 32, kWave);
+      // O^T += V^T P : P (key rows, query on lane) is the B operand as is; the
+      // V^T fragment (d on the lane, the permuted key order of P on k) comes
+      // from two hardware-transposed reads of the row-major V tile.
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int st = s >> 1, sp = s & 1;
-      bf16x8 pb;
+      for (int s = 0; s < 4; ++s) {
+        const int st = s >> 1, sp = s & 1;
+        bf16x8 pb;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[st][8 * sp + j]);
-      const int kl = st * 32 + 16 * sp + 4 * hh;
+        for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[st][8 * sp + j]);
+        const int kbase = st * 32 + 16 * sp + tr_row;
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const bf16_t* vrow = &Vt[(db * 32 + lq) * VST + kl];
-        const bf16x8 a = cat44(*reinterpret_cast<const u16x4*>(vrow),
-                               *reinterpret_cast<const u16x4*>(vrow + 8));
-        oacc[db] = mfma(a, pb, oacc[db]);
+        for (int db = 0; db < 4; ++db) {
+          const u16x4 lo = tr_read(Vc, v_off(kbase, 4 * db + tr_ch) + tr_byte);
+          const u16x4 hi = tr_read(Vc, v_off(kbase + 8, 4 * db + tr_ch) + tr_byte);
+          oacc[db] = mfma(cat44(lo, hi), pb, oacc[db]);
+        }
       }
     }
+    if (kt + 1 < ntiles) swrite(cur ^ 1);  // the buffer every wave finished last tile
+    __syncthreads();
   }
   if (qrow < S) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -245,21 +303,52 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const bf16_t* __restric
   }
 }
 
-constexpr int BQT = 32;        // query rows per backward step
-constexpr int QST = HD + 8;    // Q / dO row-image stride (bf16)
-constexpr int TST = BQT + 4;   // Q^T / dO^T image stride (bf16): 72 B rows
+constexpr int BQT = 32;               // query rows per backward step
+constexpr int QTILE = BQT * HD;       // bf16 elements of one Q (or dO) image
 
-// dK, dV: one workgroup = 128 keys of one (b, kv head); wave = 32 keys.
-__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
+// Backward LDS images use layout (a) of cdna_hip_programming.md T10: 8-row x
+// 32-column subtiles of 512 B.  Row reads (ds_read_b128) and transposed reads
+// (ds_read_b64_tr_b16) are both conflict-free as with (b), but the eight row
+// reads (t = 0..7) and the sixteen transposed reads of one 32x32x16 operand
+// differ only by immediate offsets from TWO base addresses each — the
+// register-lean choice for kernels that sit at the 256-VGPR limit.
+__device__ __forceinline__ int a_off(int row, int ch) {
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// Row read of the 16-B chunk `ch` of row `row`.
+__device__ __forceinline__ bf16x8 row_read(const bf16_t* img, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(img) + a_off(row, ch));
+}
+
+// A-operand fragment of a product that sums over the image's ROWS: two
+// hardware-transposed reads of rows base+{0..3} (+8), columns on the lane
+// (same geometry as the forward's V^T reads).
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* img, int base, int db, int tr_row, int tr_ch,
+                                          int tr_byte) {
+  const u16x4 lo = tr_read(img, a_off(base + tr_row, 4 * db + tr_ch) + tr_byte);
+  const u16x4 hi = tr_read(img, a_off(base + 8 + tr_row, 4 * db + tr_ch) + tr_byte);
+  return cat44(lo, hi);
+}
+
+// dK, dV: one workgroup = 128 keys of one (b, kv head); wave = 32 keys.  Q and
+// dO tiles (32 rows) are double-buffered in ONE layout-(b) image each: rows
+// read with ds_read_b128 for S = Q K^T and dP = dO V^T, columns read with
+// ds_read_b64_tr_b16 for dV^T += dO^T P and dK^T += Q^T dS — no transposed
+// copy is written.  Loads of tile i+1 are issued before tile i's MFMAs and
+// stored after them; one barrier per tile.
+// Register budget: <= 256 per lane so two workgroups share a CU (2 waves per
+// SIMD) — over it, hipcc parks the excess in AGPRs and moves it back and forth
+// every iteration.  K stays in VGPRs, the WG's V tile is read from LDS.
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ delta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S,
     int Hq, int Hkv, float c, float scale, int causal, int nKB) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQT * QST];
-  __shared__ __attribute__((aligned(16))) bf16_t Ds[BQT * QST];
-  __shared__ __attribute__((aligned(16))) bf16_t Qt[HD * TST];
-  __shared__ __attribute__((aligned(16))) bf16_t Dt[HD * TST];
-  __shared__ float Ls[BQT], Dl[BQT];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * QTILE];
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[2 * QTILE];
+  __shared__ __attribute__((aligned(16))) bf16_t Vw[128 * HD];  // this WG's 128 keys
+  __shared__ float Ls[2 * BQT], Dl[2 * BQT];
   const int G = Hq / Hkv;
   // Decode (b, hkv, key block): XCD-aware, heaviest (earliest keys) first.
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -271,15 +360,23 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
   const int key0 = kb * 128 + w * 32;
   const int key = key0 + lk;
   const size_t qs = static_cast<size_t>(Hq) * HD, kvs = static_cast<size_t>(Hkv) * HD;
-  bf16x8 kf[8], vf[8];
+  bf16x8 kf[8];
   {
     const size_t off = (static_cast<size_t>(b) * S + key) * kvs + static_cast<size_t>(hkv) * HD;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      kf[t] = key < S ? ld16(k + off + 16 * t + 8 * hh) : bf16x8{};
-      vf[t] = key < S ? ld16(v + off + 16 * t + 8 * hh) : bf16x8{};
+    for (int t = 0; t < 8; ++t) kf[t] = key < S ? ld16(k + off + 16 * t + 8 * hh) : bf16x8{};
+    // V rows kb*128 .. +127 -> layout-(b) image (row reads only); published
+    // by the barrier before the main loop.
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = (threadIdx.x >> 4) + 16 * i, ch = threadIdx.x & 15, s = kb * 128 + r;
+      const bf16x8 x = s < S ? ld16(v + (static_cast<size_t>(b) * S + s) * kvs +
+                                    static_cast<size_t>(hkv) * HD + ch * 8)
+                             : bf16x8{};
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Vw) + a_off(r, ch)) = x;
     }
   }
+  const bf16_t* Vmine = Vw + w * 32 * HD;  // a_off: a 32-row slice is a whole number of subtiles
   f32x16 dka[4], dva[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) dka[i] = dva[i] = f32x16{};
@@ -287,6 +384,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
   const int qt_begin = causal ? (kb * 128) / BQT : 0;
   const int nqt = (S + BQT - 1) / BQT;
   const int total = G * (nqt - qt_begin);
+  // Staging: thread t moves row chunks (r, ch) = ((t + 256 i) >> 4, t & 15), i = 0, 1.
+  const int sr = threadIdx.x >> 4, sch = threadIdx.x & 15;
   bf16x8 qr[2], dr[2];
   float lr = 0.f, drl = 0.f;
   auto gload = [&](int it) {
@@ -294,8 +393,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
     const int h = hkv * G + g;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int idx = threadIdx.x + 256 * i, r = idx >> 4, ch = idx & 15, s = qt * BQT + r;
-      const size_t off = (static_cast<size_t>(b) * S + s) * qs + static_cast<size_t>(h) * HD + ch * 8;
+      const int s = qt * BQT + sr + 16 * i;
+      const size_t off = (static_cast<size_t>(b) * S + s) * qs + static_cast<size_t>(h) * HD + sch * 8;
       qr[i] = s < S ? ld16(q + off) : bf16x8{};
       dr[i] = s < S ? ld16(dout + off) : bf16x8{};
     }
@@ -306,67 +405,73 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
       drl = s < S ? delta[li] : 0.f;
     }
   };
-  if (total > 0) gload(0);
-  for (int it = 0; it < total; ++it) {
-    const int qt = qt_begin + it % (nqt - qt_begin);
-    __syncthreads();
+  auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int idx = threadIdx.x + 256 * i, r = idx >> 4, ch = idx & 15;
-      *reinterpret_cast<bf16x8*>(&Qs[r * QST + ch * 8]) = qr[i];
-      *reinterpret_cast<bf16x8*>(&Ds[r * QST + ch * 8]) = dr[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Qt[(ch * 8 + j) * TST + r] = qr[i][j];
-        Dt[(ch * 8 + j) * TST + r] = dr[i][j];
-      }
+      const int off = a_off(sr + 16 * i, sch);
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Qs + buf * QTILE) + off) = qr[i];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Ds + buf * QTILE) + off) = dr[i];
     }
     if (threadIdx.x < BQT) {
-      Ls[threadIdx.x] = lr;
-      Dl[threadIdx.x] = drl;
+      Ls[buf * BQT + threadIdx.x] = lr;
+      Dl[buf * BQT + threadIdx.x] = drl;
     }
-    __syncthreads();
+  };
+  const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
+  const int tr_row = 4 * (trG >> 1) + trq, tr_ch = 2 * (trG & 1) + (trp >> 1), tr_byte = 8 * (trp & 1);
+  if (total > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    const int qt = qt_begin + it % (nqt - qt_begin);
     if (it + 1 < total) gload(it + 1);
     const int qbase = qt * BQT;
-    if (causal && qbase + BQT - 1 < key0) continue;  // every query of this tile precedes our keys
-    // S[q][key] = Q K^T and dP[q][key] = dO V^T (key on the lane).
-    f32x16 sa = f32x16{}, pa = f32x16{};
+    if (!causal || qbase + BQT - 1 >= key0) {  // else every query of this tile precedes our keys
+      const bf16_t* Qc = Qs + cur * QTILE;
+      const bf16_t* Dc = Ds + cur * QTILE;
+      const float* Lc = Ls + cur * BQT;
+      const float* Dlc = Dl + cur * BQT;
+      // S[q][key] = Q K^T and dP[q][key] = dO V^T (key on the lane).
+      f32x16 sa = f32x16{}, pa = f32x16{};
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      sa = mfma(*reinterpret_cast<const bf16x8*>(&Qs[lk * QST + 16 * t + 8 * hh]), kf[t], sa);
-      pa = mfma(*reinterpret_cast<const bf16x8*>(&Ds[lk * QST + 16 * t + 8 * hh]), vf[t], pa);
-    }
-    // P = exp2(S c - lse2), dS = P (dP - delta); row r <-> query qbase + acc_row(r).
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qi = acc_row(r, hh);
-      const int qrow = qbase + qi;
-      float p = exp2f(sa[r] * c - Ls[qi]);
-      if (key >= S || qrow >= S || (causal && key > qrow)) p = 0.f;
-      sa[r] = p;
-      pa[r] = p * (pa[r] - Dl[qi]);
-    }
-    // dV^T += dO^T P ; dK^T += Q^T dS   (P, dS as B operands, permuted q order)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 pb, sb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        pb[j] = f2bf(sa[8 * s + j]);
-        sb[j] = f2bf(pa[8 * s + j]);
+      for (int t = 0; t < 8; ++t) {
+        sa = mfma(row_read(Qc, lk, 2 * t + hh), kf[t], sa);
+        pa = mfma(row_read(Dc, lk, 2 * t + hh), row_read(Vmine, lk, 2 * t + hh), pa);
       }
-      const int ql = 16 * s + 4 * hh;
+      // P = exp2(S c - lse2), dS = P (dP - delta); row r <-> query qbase + acc_row(r).
+      const bool edge = (causal && key0 + 31 > qbase) || qbase + BQT > S || key0 + 32 > S;
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const bf16_t* drow = &Dt[(db * 32 + lk) * TST + ql];
-        const bf16_t* qrow_t = &Qt[(db * 32 + lk) * TST + ql];
-        dva[db] = mfma(cat44(*reinterpret_cast<const u16x4*>(drow), *reinterpret_cast<const u16x4*>(drow + 8)),
-                       pb, dva[db]);
-        dka[db] = mfma(cat44(*reinterpret_cast<const u16x4*>(qrow_t),
-                             *reinterpret_cast<const u16x4*>(qrow_t + 8)),
-                       sb, dka[db]);
+      for (int r = 0; r < 16; ++r) {
+        const int qi = acc_row(r, hh);
+        float p = exp2f(sa[r] * c - Lc[qi]);
+        if (edge) {
+          const int qrow = qbase + qi;
+          if (key >= S || qrow >= S || (causal && key > qrow)) p = 0.f;
+        }
+        sa[r] = p;
+        pa[r] = p * (pa[r] - Dlc[qi]);
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS   (P, dS as B operands, permuted q order)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = f2bf(sa[8 * s + j]);
+          sb[j] = f2bf(pa[8 * s + j]);
+        }
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          dva[db] = mfma(tr_frag(Dc, 16 * s, db, tr_row, tr_ch, tr_byte), pb, dva[db]);
+          dka[db] = mfma(tr_frag(Qc, 16 * s, db, tr_row, tr_ch, tr_byte), sb, dka[db]);
+        }
       }
     }
+    if (it + 1 < total) swrite(cur ^ 1);
+    __syncthreads();
   }
   if (key < S) {
     const size_t off = (static_cast<size_t>(b) * S + key) * kvs + static_cast<size_t>(hkv) * HD;
@@ -387,15 +492,16 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
 }
 
 // dQ: one workgroup = 128 query rows of one (b, head); wave = 32 rows (the
-// forward's geometry: query on the lane).
-__global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(
+// forward's geometry: query on the lane).  K and V tiles double-buffered in
+// layout-(b) images: K rows for S^T = K Q^T and K columns (transposed reads)
+// for dQ^T += K^T dS^T from the same image; V rows for dP^T = V dO^T.
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ delta, bf16_t* __restrict__ dq, int S, int Hq, int Hkv, float c,
     float scale, int causal, int nQB) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * KST];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * KST];
-  __shared__ __attribute__((aligned(16))) bf16_t Kt[HD * VST];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * VTILE];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * VTILE];
   int b, h, hkv, qb;
   decode(nQB, Hq / Hkv, Hkv, causal, &b, &h, &hkv, &qb);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -422,62 +528,71 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(
   const int ntiles = (kv_end + BKV - 1) / BKV;
   const bf16_t* kb_ = k + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
   const bf16_t* vb_ = v + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
+  // Staging: thread t moves chunks (key, ch) = ((t + 256 i) >> 4, t & 15), i = 0..3.
+  const int skey = threadIdx.x >> 4, sch = threadIdx.x & 15;
   bf16x8 kr[4], vr[4];
   auto gload = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = threadIdx.x + 256 * i, kk = idx >> 4, ch = idx & 15, s = kt * BKV + kk;
-      kr[i] = s < S ? ld16(kb_ + static_cast<size_t>(s) * kvs + ch * 8) : bf16x8{};
-      vr[i] = s < S ? ld16(vb_ + static_cast<size_t>(s) * kvs + ch * 8) : bf16x8{};
+      const int s = kt * BKV + skey + 16 * i;
+      kr[i] = s < S ? ld16(kb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
+      vr[i] = s < S ? ld16(vb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
     }
   };
-  gload(0);
-  for (int kt = 0; kt < ntiles; ++kt) {
-    __syncthreads();
+  auto swrite = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = threadIdx.x + 256 * i, kk = idx >> 4, ch = idx & 15;
-      *reinterpret_cast<bf16x8*>(&Ks[kk * KST + ch * 8]) = kr[i];
-      *reinterpret_cast<bf16x8*>(&Vs[kk * KST + ch * 8]) = vr[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Kt[(ch * 8 + j) * VST + kk] = kr[i][j];
+      const int off = a_off(skey + 16 * i, sch);
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Ks + buf * VTILE) + off) = kr[i];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Vs + buf * VTILE) + off) = vr[i];
     }
-    __syncthreads();
+  };
+  const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
+  const int tr_row = 4 * (trG >> 1) + trq, tr_ch = 2 * (trG & 1) + (trp >> 1), tr_byte = 8 * (trp & 1);
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
     if (kt + 1 < ntiles) gload(kt + 1);
     const int k0 = kt * BKV;
-    if (causal && k0 > q0 + 31) continue;
-    f32x16 sa[2] = {f32x16{}, f32x16{}}, pa[2] = {f32x16{}, f32x16{}};
+    if (!causal || k0 <= q0 + 31) {
+      const bf16_t* Kc = Ks + cur * VTILE;
+      const bf16_t* Vc = Vs + cur * VTILE;
+      const bool edge = (causal && k0 + BKV - 1 > q0) || k0 + BKV > S || q0 + 32 > S;
+      // Two 32-key halves in sequence: one S^T / dP^T accumulator pair live
+      // at a time keeps the kernel inside 256 VGPRs.
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+      for (int st = 0; st < 2; ++st) {
+        f32x16 sa = f32x16{}, pa = f32x16{};
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        sa[st] = mfma(*reinterpret_cast<const bf16x8*>(&Ks[(st * 32 + lq) * KST + 16 * t + 8 * hh]), qf[t], sa[st]);
-        pa[st] = mfma(*reinterpret_cast<const bf16x8*>(&Vs[(st * 32 + lq) * KST + 16 * t + 8 * hh]), df[t], pa[st]);
-      }
+        for (int t = 0; t < 8; ++t) {
+          sa = mfma(row_read(Kc, st * 32 + lq, 2 * t + hh), qf[t], sa);
+          pa = mfma(row_read(Vc, st * 32 + lq, 2 * t + hh), df[t], pa);
+        }
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(sa[r] * c - my_lse);
+          if (edge) {
+            const int kk = k0 + st * 32 + acc_row(r, hh);
+            if (kk >= S || qrow >= S || (causal && kk > qrow)) p = 0.f;
+          }
+          pa[r] = p * (pa[r] - my_delta);  // dS^T
+        }
+        // dQ^T += K^T dS^T
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = k0 + st * 32 + acc_row(r, hh);
-        float p = exp2f(sa[st][r] * c - my_lse);
-        if (kk >= S || qrow >= S || (causal && kk > qrow)) p = 0.f;
-        pa[st][r] = p * (pa[st][r] - my_delta);  // dS^T
-      }
-    // dQ^T += K^T dS^T
+        for (int sp = 0; sp < 2; ++sp) {
+          bf16x8 sb;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int st = s >> 1, sp = s & 1;
-      bf16x8 sb;
+          for (int j = 0; j < 8; ++j) sb[j] = f2bf(pa[8 * sp + j]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sb[j] = f2bf(pa[st][8 * sp + j]);
-      const int kl = st * 32 + 16 * sp + 4 * hh;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const bf16_t* krow = &Kt[(db * 32 + lq) * VST + kl];
-        dqa[db] = mfma(cat44(*reinterpret_cast<const u16x4*>(krow), *reinterpret_cast<const u16x4*>(krow + 8)),
-                       sb, dqa[db]);
+          for (int db = 0; db < 4; ++db)
+            dqa[db] = mfma(tr_frag(Kc, st * 32 + 16 * sp, db, tr_row, tr_ch, tr_byte), sb, dqa[db]);
+        }
       }
     }
+    if (kt + 1 < ntiles) swrite(cur ^ 1);
+    __syncthreads();
   }
   if (qrow < S) {
     bf16_t* p = dq + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
@@ -530,11 +645,11 @@ KGWE_API int kgwe_flash_attn_fwd(const void* q, const void* k, const void* v, vo
                                  int B, int S, int Hq, int Hkv, int D, float scale, int causal,
                                  hipStream_t s) {
   if (D != HD || Hq % Hkv != 0 || B <= 0 || S <= 0) return -1;
-  const int nQB = (S + BQ - 1) / BQ;
+  const int nQB = (S + BQF - 1) / BQF;
   const long long grid = static_cast<long long>(B) * Hq * nQB;
   if (grid > 0x7fffffff) return -1;
   const float c = scale * 1.4426950408889634f;  // softmax in the exp2 domain
-  hipLaunchKernelGGL(fa_fwd_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, s,
+  hipLaunchKernelGGL(fa_fwd_kernel, dim3(static_cast<unsigned>(grid)), dim3(512), 0, s,
                      static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
                      static_cast<const bf16_t*>(v), static_cast<bf16_t*>(o), lse2, S, Hq, Hkv, c,
                      causal, nQB);
