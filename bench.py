@@ -143,6 +143,7 @@ def main(argv=None) -> int:
             "peak_mem_gb_rank0": round(res.peak_mem_gb, 1),
             "attention": "sdpa" if (args.sdpa or not attn_ops.hip_flash_available())
             else "kgwe_flash_attn",
+            "gemm_solutions": "tuned (kgwe/tuning)" if tr.tuned_gemms else "library default",
         }
         print(json.dumps(out), flush=True)
     kdist.barrier(info)

@@ -19,6 +19,7 @@ from ..ops import FusedAdamW
 from ..parallel import dist as kdist
 from ..parallel.fsdp import shard_model
 from ..parallel.zero import ShardedDataParallel
+from ..utils import gemm_tuning
 from ..utils.amdsmi_util import UtilSampler
 
 
@@ -58,6 +59,9 @@ class Trainer:
         self.model.activation_checkpointing = tc.activation_checkpointing
         self.opt = None
         self.dp = None
+        self.tuned_gemms = dev.type == "cuda" and gemm_tuning.enable()
+        if self.tuned_gemms:
+            log(info, f"GEMM solutions pinned from {gemm_tuning.RESULTS.name}")
         if tc.parallel == "fsdp":
             if not torch.distributed.is_initialized():
                 raise RuntimeError("FSDP needs a process group: kdist.init(force_group=True)")

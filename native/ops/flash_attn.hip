@@ -348,7 +348,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * QTILE];
   __shared__ __attribute__((aligned(16))) bf16_t Ds[2 * QTILE];
   __shared__ __attribute__((aligned(16))) bf16_t Vw[128 * HD];  // this WG's 128 keys
-  __shared__ float Ls[2 * BQT], Dl[2 * BQT];
+  __shared__ __attribute__((aligned(16))) float Ls[2 * BQT];
+  __shared__ __attribute__((aligned(16))) float Dl[2 * BQT];
   const int G = Hq / Hkv;
   // Decode (b, hkv, key block): XCD-aware, heaviest (earliest keys) first.
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   bf16x8 qr[2], dr[2];
   float lr = 0.f, drl = 0.f;
   auto gload = [&](int it) {
-    const int g = it / (nqt - qt_begin), qt = qt_begin + it % (nqt - qt_begin);
+    const int g = it % G, qt = nqt - 1 - it / G;
     const int h = hkv * G + g;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -426,7 +427,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   __syncthreads();
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
-    const int qt = qt_begin + it % (nqt - qt_begin);
+    // Query tiles from the LAST one down, heads innermost: every key block of
+    // a (batch, kv head) — all resident on one XCD — reads the same Q / dO
+    // tile at the same time (one L2 fill, not one per key block); a block
+    // stops when the sweep passes its diagonal.
+    const int qt = nqt - 1 - it / G;
     if (it + 1 < total) gload(it + 1);
     const int qbase = qt * BQT;
     if (!causal || qbase + BQT - 1 >= key0) {  // else every query of this tile precedes our keys
@@ -444,15 +449,21 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
       // P = exp2(S c - lse2), dS = P (dP - delta); row r <-> query qbase + acc_row(r).
       const bool edge = (causal && key0 + 31 > qbase) || qbase + BQT > S || key0 + 32 > S;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = acc_row(r, hh);
-        float p = exp2f(sa[r] * c - Lc[qi]);
-        if (edge) {
-          const int qrow = qbase + qi;
-          if (key >= S || qrow >= S || (causal && key > qrow)) p = 0.f;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        // accumulator rows 4*g4 .. +3 are queries 8*g4 + 4*hh + 0..3: one b128 read each
+        const f32x4 lse4 = *reinterpret_cast<const f32x4*>(Lc + 8 * g4 + 4 * hh);
+        const f32x4 del4 = *reinterpret_cast<const f32x4*>(Dlc + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g4 + j;
+          float p = exp2f(sa[r] * c - lse4[j]);
+          if (edge) {
+            const int qrow = qbase + acc_row(r, hh);
+            if (key >= S || qrow >= S || (causal && key > qrow)) p = 0.f;
+          }
+          sa[r] = p;
+          pa[r] = p * (pa[r] - del4[j]);
         }
-        sa[r] = p;
-        pa[r] = p * (pa[r] - Dlc[qi]);
       }
       // dV^T += dO^T P ; dK^T += Q^T dS   (P, dS as B operands, permuted q order)
 #pragma unroll
