@@ -42,11 +42,10 @@ _SIGS = {
                                        c_int64, c_void_p]),
     "kgwe_cross_entropy_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int64, c_int64, c_int64, c_void_p]),
-    "kgwe_adamw_step": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_float,
+    "kgwe_adamw_step": (c_int, [c_void_p, c_int, c_float, c_float, c_float, c_float,
                                 c_float, c_int, c_float, c_void_p]),
     "kgwe_adamw_chunk_elems": (c_int, []),
     "kgwe_adamw_tensor_bytes": (c_int, []),
-    "kgwe_adamw_chunk_bytes": (c_int, []),
 }
 _OPTIONAL_SIGS = {
     "kgwe_flash_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

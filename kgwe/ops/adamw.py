@@ -8,9 +8,9 @@
   replicated-weights mixed-precision path (288 GB of HBM holds bf16 weights,
   fp32 master and both moments of an 8B model with room for activations).
 
-On a GPU the ``kgwe_adamw_step`` HIP kernel does every tensor in one launch;
-the pointer/chunk tables (``AdamPlan``) are rebuilt only when some storage
-moves.  On CPU the fp32 reference is used.
+On a GPU the ``kgwe_adamw_step`` HIP kernel updates 16 tensors per launch
+with their pointers passed by value (no device tables).  On CPU the fp32
+reference is used.
 """
 from __future__ import annotations
 
@@ -22,7 +22,6 @@ from ._lib import check, lib, stream
 
 _TENSOR_DT = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"),
                        ("shadow", "<u8"), ("n", "<i8"), ("g_bf16", "<i4"), ("pad", "<i4")])
-_CHUNK_DT = np.dtype([("tensor", "<i4"), ("pad", "<i4"), ("start", "<i8")])
 
 
 def _local(t: torch.Tensor) -> torch.Tensor:
@@ -30,63 +29,51 @@ def _local(t: torch.Tensor) -> torch.Tensor:
 
 
 class AdamPlan:
-    """Pointer + chunk tables for one multi-tensor AdamW launch.
+    """Launcher for the multi-tensor AdamW kernel.
 
     ``entries`` = [(p fp32, g fp32|bf16, m fp32, v fp32, shadow bf16|None)], all
     contiguous with equal element counts (checked on the host: the kernel
-    trusts the table)."""
+    trusts the records).  The pointer records go to the kernel by value (16
+    per launch), so a launch costs one small numpy record array on the host
+    and nothing on the device — cheap enough to issue per gradient bucket."""
 
-    def __init__(self):
-        self._key = None
-        self._dev = None
+    _size_checked = False
 
     @staticmethod
     def _check(i, p, g, m, v, sh):
         ok = (p.dtype == m.dtype == v.dtype == torch.float32
               and g.dtype in (torch.float32, torch.bfloat16)
               and all(t.is_contiguous() for t in (p, g, m, v))
-              and p.numel() == g.numel() == m.numel() == v.numel()
+              and p.numel() == g.numel() == m.numel() == v.numel() > 0
+              and all(t.device == p.device for t in (g, m, v))
               and (sh is None or (sh.dtype == torch.bfloat16 and sh.is_contiguous()
-                                  and sh.numel() == p.numel())))
+                                  and sh.numel() == p.numel() and sh.device == p.device)))
         if not ok:
             raise ValueError(f"AdamW: entry {i} violates the kernel contract "
                              f"(p {p.dtype}/{tuple(p.shape)}, g {g.dtype}/{tuple(g.shape)}, "
                              f"shadow {None if sh is None else (sh.dtype, tuple(sh.shape))})")
 
-    def _tables(self, entries):
-        key = tuple((p.data_ptr(), g.data_ptr(), g.dtype == torch.bfloat16) for p, g, *_ in entries)
-        if key == self._key:
-            return self._dev
+    @classmethod
+    def records(cls, entries) -> np.ndarray:
         L = lib()
-        chunk = L.kgwe_adamw_chunk_elems()
-        assert L.kgwe_adamw_tensor_bytes() == _TENSOR_DT.itemsize
+        if not AdamPlan._size_checked:
+            assert L.kgwe_adamw_tensor_bytes() == _TENSOR_DT.itemsize
+            AdamPlan._size_checked = True
         tens = np.zeros(len(entries), dtype=_TENSOR_DT)
-        chunks = []
         for i, (p, g, m, v, sh) in enumerate(entries):
-            self._check(i, p, g, m, v, sh)
+            cls._check(i, p, g, m, v, sh)
             tens[i] = (p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
                        0 if sh is None else sh.data_ptr(), p.numel(),
                        int(g.dtype == torch.bfloat16), 0)
-            chunks.extend((i, 0, s) for s in range(0, p.numel(), chunk))
-        ch = np.array(chunks, dtype=_CHUNK_DT)
-        dev = entries[0][0].device
-        # Pinned staging + async H2D on the compute stream: no host sync.  The
-        # staging buffers stay referenced until the next rebuild, long after
-        # the stream consumed them.
-        t_host = torch.from_numpy(tens.view(np.uint8).copy()).pin_memory()
-        c_host = torch.from_numpy(ch.view(np.uint8).copy()).pin_memory()
-        self._dev = (t_host.to(dev, non_blocking=True), c_host.to(dev, non_blocking=True),
-                     len(chunks), t_host, c_host)
-        self._key = key
-        return self._dev
+        return tens
 
     def launch(self, entries, lr, b1, b2, eps, wd, step, grad_scale=1.0):
         if not entries:
             return
         p0 = entries[0][0]
         if p0.is_cuda:
-            t_dev, c_dev, n = self._tables(entries)[:3]
-            check(lib().kgwe_adamw_step(t_dev.data_ptr(), c_dev.data_ptr(), n, lr, b1, b2, eps, wd,
+            tens = self.records(entries)
+            check(lib().kgwe_adamw_step(tens.ctypes.data, len(entries), lr, b1, b2, eps, wd,
                                         step, grad_scale, stream(p0)), "adamw_step")
             return
         for p, g, m, v, sh in entries:

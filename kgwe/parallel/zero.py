@@ -13,20 +13,23 @@ gradient (ZeRO-2):
   bucket's fp32 (or bf16) gradient buffer and frees it; when a bucket is
   complete its **reduce-scatter** is issued asynchronously over RCCL, so the
   collectives of early buckets overlap the rest of backward;
-* step: one multi-tensor HIP AdamW launch over this rank's shards (fp32
-  master, m, v; grads averaged through ``grad_scale``) writes the rounded
-  bf16 result straight into this rank's slice of each bucket, then one
-  in-place **all-gather** per bucket re-replicates the weights; the next
-  forward waits for a bucket's all-gather only in the pre-hook of the first
-  module that reads it, so the gathers overlap the start of the forward.
+* update, per bucket, as soon as the bucket's gradients are reduced — still
+  inside backward, on a side HIP stream: a multi-tensor HIP AdamW launch over
+  this rank's shard (fp32 master, m, v; grads averaged through
+  ``grad_scale``) writes the rounded bf16 result straight into this rank's
+  slice of the bucket, then an in-place **all-gather** re-replicates the
+  weights.  The HBM-bound optimizer and the collectives thus run beside the
+  MFMA-bound backward GEMMs; the next forward waits for a bucket only in the
+  pre-hook of the first module that reads it.
 
 Per step and per GPU that is one reduce-scatter of the gradients and one
 all-gather of the bf16 weights — FSDP's volume with reshard_after_forward off
 — in ~2 x (params / bucket) large collectives, the shape ring collectives
 over point-to-point xGMI links want.
 
-With one rank there is no communication at all: AdamW reads autograd's bf16
-gradients in place and writes the bf16 weights the next forward reads — no
+With one rank there is no communication at all: AdamW (still per bucket,
+from the backward hooks) reads autograd's bf16 gradients in place and
+writes the bf16 weights the next forward reads — no
 cast, copy or all-gather-copy kernels (the FSDP2 path spends ~90 ms/step on
 those at 1 GPU for Llama-3-8B, profiles/r01_pack).
 
@@ -36,6 +39,8 @@ training-side implementation the platform places.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -44,25 +49,42 @@ from ..ops.adamw import AdamPlan
 
 class _Bucket:
     __slots__ = ("params", "offsets", "numel", "padded", "shard", "flat", "master", "m", "v",
-                 "gfull", "gshard", "pending", "seen", "rs_work", "ag_work")
+                 "gfull", "gshard", "pending", "seen", "rs_work", "ag_work", "ready", "updated")
 
 
 class ShardedDataParallel:
+    """overlap_step=True (default): each bucket's optimizer update is issued
+    from the backward hook that completes the bucket, on a side HIP stream —
+    world 1: AdamW straight from autograd's bf16 gradients; world N:
+    reduce-scatter (compute-stream order) -> AdamW on the shard -> in-place
+    all-gather, chained on the side / RCCL streams — so the HBM-bound AdamW
+    and the collectives run under the rest of backward's MFMA-bound GEMMs,
+    and only the last bucket's update is exposed.  A bucket's weights are free
+    to change once its gradients are complete: every backward op that reads
+    a weight (dX = dY W) runs in the same autograd node that produces that
+    weight's gradient, before the accumulate-grad hook fires.  This assumes
+    each parameter receives ONE gradient per backward (no weight tying).
+    The next forward waits per bucket in a module pre-hook."""
+
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, bucket_elems: int = 100 * 2**20,
-                 reduce_dtype: torch.dtype = torch.float32, group=None):
+                 reduce_dtype: torch.dtype = torch.float32, group=None, overlap_step: bool = True):
         self.model = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.reduce_dtype = reduce_dtype
+        self.overlap = overlap_step
         self._step = 0
+        self._armed = False  # this iteration's step counter already advanced
         self._plan = AdamPlan()
         params = [p for p in model.parameters() if p.requires_grad]
         if not params:
             raise ValueError("ShardedDataParallel: model has no trainable parameters")
         self.device = params[0].device
+        self._side = (torch.cuda.Stream(self.device)
+                      if self.device.type == "cuda" and (self.overlap or self.world > 1) else None)
         self.buckets: list[_Bucket] = []
         cur: list[torch.nn.Parameter] = []
         n = 0
@@ -76,7 +98,7 @@ class ShardedDataParallel:
         self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
         self._slot = {id(p): (b, o) for b in self.buckets for p, o in zip(b.params, b.offsets)}
         self._hooks = []
-        if self.world > 1:
+        if self.world > 1 or self.overlap:
             for b in self.buckets:
                 for p in b.params:
                     self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready))
@@ -86,7 +108,7 @@ class ShardedDataParallel:
                 if own:
                     uniq = list({id(b): b for b in own}.values())
                     self._hooks.append(mod.register_forward_pre_hook(
-                        lambda _m, _a, bs=uniq: self._wait_gather(bs)))
+                        lambda _m, _a, bs=uniq: self._wait_params(bs)))
 
     # ------------------------------------------------------------ layout
     def _make_bucket(self, params) -> _Bucket:
@@ -122,73 +144,115 @@ class ShardedDataParallel:
         b.seen = set()
         b.rs_work = None
         b.ag_work = None
+        b.ready = None
+        b.updated = False
         return b
 
     # ------------------------------------------------------------ backward
     @torch.no_grad()
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
         b, o = self._slot[id(p)]
-        b.gfull[o:o + p.numel()].view(p.shape).copy_(p.grad)
-        p.grad = None
+        if self.world > 1:
+            b.gfull[o:o + p.numel()].view(p.shape).copy_(p.grad)
+            p.grad = None
         if id(p) not in b.seen:
             b.seen.add(id(p))
             b.pending -= 1
             if b.pending == 0:
-                self._reduce_scatter(b)
+                self._bucket_complete(b)
+
+    def _bucket_complete(self, b: _Bucket) -> None:
+        if not self._armed:
+            self._step += 1
+            self._armed = True
+        if self.world > 1:
+            self._reduce_scatter(b)
+        if self.overlap:
+            self._update(b)
 
     def _reduce_scatter(self, b: _Bucket) -> None:
         b.rs_work = dist.reduce_scatter_tensor(b.gshard, b.gfull, op=dist.ReduceOp.SUM,
                                                group=self.group, async_op=True)
 
-    def _wait_gather(self, buckets) -> None:
+    @torch.no_grad()
+    def _update(self, b: _Bucket) -> None:
+        """AdamW on this rank's part of bucket ``b`` (+ all-gather for world
+        > 1), on the side stream when there is one."""
+        b1, b2 = self.betas
+        side = self._side
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            ctx = torch.cuda.stream(side)
+        else:
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if self.world > 1:
+                b.rs_work.wait()
+                b.rs_work = None
+                s0 = self.rank * b.shard
+                self._plan.launch([(b.master, b.gshard, b.m, b.v, b.flat[s0:s0 + b.shard])],
+                                  self.lr, b1, b2, self.eps, self.wd, self._step,
+                                  grad_scale=1.0 / self.world)
+                b.ag_work = dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard],
+                                                        group=self.group, async_op=True)
+            else:
+                entries = []
+                for p, o in zip(b.params, b.offsets):
+                    g = p.grad
+                    if g is None:
+                        continue
+                    g = g if g.is_contiguous() else g.contiguous()
+                    if side is not None:
+                        g.record_stream(side)  # freed by autograd's stream, read here
+                    n = p.numel()
+                    entries.append((b.master[o:o + n], g.view(-1), b.m[o:o + n], b.v[o:o + n],
+                                    b.flat[o:o + n]))
+                    p.grad = None
+                self._plan.launch(entries, self.lr, b1, b2, self.eps, self.wd, self._step)
+                if side is not None:
+                    b.ready = torch.cuda.Event()
+                    b.ready.record(side)
+        b.updated = True
+
+    def _wait_params(self, buckets) -> None:
         for b in buckets:
             if b.ag_work is not None:
                 b.ag_work.wait()
                 b.ag_work = None
+            if b.ready is not None:
+                torch.cuda.current_stream(self.device).wait_event(b.ready)
+                b.ready = None
 
     def wait_params(self) -> None:
-        """Block (the current stream) until every bucket's weights are gathered —
-        call before reading parameters outside a forward (eval, checkpoint)."""
-        self._wait_gather(self.buckets)
+        """Make the current stream wait until every bucket's weights are
+        updated and gathered — call before reading parameters outside a
+        forward (eval, checkpoint)."""
+        self._wait_params(self.buckets)
 
     # ------------------------------------------------------------ step
     @torch.no_grad()
     def step(self) -> None:
-        self._step += 1
-        b1, b2 = self.betas
-        entries = []
-        if self.world == 1:
-            for b in self.buckets:
-                for p, o in zip(b.params, b.offsets):
-                    if p.grad is None:
-                        continue
-                    n = p.numel()
-                    g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                    entries.append((b.master[o:o + n], g.view(-1), b.m[o:o + n], b.v[o:o + n],
-                                    b.flat[o:o + n]))
-            self._plan.launch(entries, self.lr, b1, b2, self.eps, self.wd, self._step)
-            for b in self.buckets:
-                for p in b.params:
-                    p.grad = None
-            return
-        for b in self.buckets:
-            if b.rs_work is None:  # some parameter got no gradient this step
+        """Finish the optimizer step: update the buckets no backward hook
+        completed (overlap off, or parameters that got no gradient)."""
+        if not self._armed:
+            self._step += 1
+        # Gather order: the next forward reads buckets in reverse (they are in
+        # backward order) and collectives on one RCCL stream complete in issue
+        # order, so the embedding / first layers' bucket goes first.
+        for b in reversed(self.buckets):
+            if b.updated:
+                continue
+            if self.world > 1 and b.rs_work is None:  # some parameter got no gradient
                 for p, o in zip(b.params, b.offsets):
                     if id(p) not in b.seen:
                         b.gfull[o:o + p.numel()].zero_()
                 self._reduce_scatter(b)
-            b.rs_work.wait()
-            b.rs_work = None
+            self._update(b)
+        for b in self.buckets:
             b.pending = len(b.params)
             b.seen.clear()
-            s0 = self.rank * b.shard
-            entries.append((b.master, b.gshard, b.m, b.v, b.flat[s0:s0 + b.shard]))
-        self._plan.launch(entries, self.lr, b1, b2, self.eps, self.wd, self._step,
-                          grad_scale=1.0 / self.world)
-        for b in self.buckets:
-            s0 = self.rank * b.shard
-            b.ag_work = dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard],
-                                                    group=self.group, async_op=True)
+            b.updated = False
+        self._armed = False
 
     def zero_grad(self) -> None:
         for b in self.buckets:

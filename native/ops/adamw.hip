@@ -1,15 +1,16 @@
 // Multi-tensor fused AdamW for fp32 master parameters.
 //
-// One launch updates every parameter (or every optimizer-state shard): the
-// host builds a chunk table (tensor index, element offset) once, the
-// per-tensor pointer table is a small device array refreshed only when
-// gradient storage moves.  Each lane streams 4 elements (16 B fp32 of p, m, v;
+// Each launch updates up to 16 parameters (or optimizer-state shards) whose
+// pointers travel in the kernel arguments, so a launch needs no device-side
+// table and can be issued per gradient bucket from a backward hook (the
+// optimizer step then overlaps the rest of backward on a side stream — see
+// kgwe/parallel/zero.py).  Each lane streams 4 elements (16 B fp32 of p, m, v;
 // 16 B fp32 or 8 B bf16 of g) and writes back p, m, v plus an optional bf16
 // copy of p — the live bf16 model weight the next forward reads.  That copy is
 // what removes the separate cast/all-gather-copy pass of a master-weight
 // scheme, and reading bf16 gradients straight from autograd's output removes
 // the fp32 up-cast pass.  HBM-bound (26-30 B/param), so the only goals are
-// full-width coalesced access and a single launch.
+// full-width coalesced access and few launches.
 //
 //   m = b1 m + (1-b1) g ;  v = b2 v + (1-b2) g^2
 //   p = p - lr * (m / bc1 / (sqrt(v / bc2) + eps) + wd * p)
@@ -26,12 +27,6 @@ struct AdamTensor {
   int64_t n;
   int32_t g_bf16;
   int32_t pad;
-};
-
-struct AdamChunk {
-  int tensor;
-  int pad;
-  int64_t start;
 };
 
 constexpr int kChunk = 256 * 4 * 16;  // elements per workgroup task (64 KiB fp32)
@@ -104,15 +99,31 @@ __device__ __forceinline__ void adam_range(const AdamTensor& t, int64_t start, i
   }
 }
 
-__global__ __launch_bounds__(256) void adamw_kernel(
-    const AdamTensor* __restrict__ tensors, const AdamChunk* __restrict__ chunks,
-    int nchunks, AdamArgs a) {
-  for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-    const AdamChunk ch = chunks[ci];
-    const AdamTensor t = tensors[ch.tensor];
-    const int64_t end = (ch.start + kChunk < t.n) ? ch.start + kChunk : t.n;
-    if (t.g_bf16) adam_range<true>(t, ch.start, end, a);
-    else adam_range<false>(t, ch.start, end, a);
+// Up to kBatch tensors per launch, passed BY VALUE in the kernel arguments
+// (~0.9 KB of the 4 KB argument space): no device-side pointer/chunk tables,
+// no H2D copy, nothing to cache when autograd hands out fresh gradient
+// buffers every step.  Workgroup task ci belongs to the first tensor whose
+// cumulative chunk count exceeds ci (linear scan over <= 16 entries).
+constexpr int kBatch = 16;
+
+struct AdamBatch {
+  AdamTensor t[kBatch];
+  int64_t chunk_end[kBatch];  // inclusive prefix sum of per-tensor chunk counts
+  int n;
+  int pad;
+};
+
+__global__ __launch_bounds__(256) void adamw_kernel(const AdamBatch b, AdamArgs a) {
+  const int64_t total = b.chunk_end[b.n - 1];
+  for (int64_t ci = blockIdx.x; ci < total; ci += gridDim.x) {
+    int i = 0;
+    while (ci >= b.chunk_end[i]) ++i;
+    const int64_t first = i ? b.chunk_end[i - 1] : 0;
+    const AdamTensor& t = b.t[i];
+    const int64_t start = (ci - first) * kChunk;
+    const int64_t end = (start + kChunk < t.n) ? start + kChunk : t.n;
+    if (t.g_bf16) adam_range<true>(t, start, end, a);
+    else adam_range<false>(t, start, end, a);
   }
 }
 
@@ -120,22 +131,34 @@ __global__ __launch_bounds__(256) void adamw_kernel(
 
 KGWE_API int kgwe_adamw_chunk_elems() { return kChunk; }
 KGWE_API int kgwe_adamw_tensor_bytes() { return sizeof(AdamTensor); }
-KGWE_API int kgwe_adamw_chunk_bytes() { return sizeof(AdamChunk); }
 
+// `tensors`: HOST array of n AdamTensor records (device pointers inside).
 // `step` is the 1-based step count after increment (bias corrections are
-// computed here on the host side of the launch; no device sync).
-KGWE_API int kgwe_adamw_step(const void* tensors, const void* chunks, int nchunks,
-                             float lr, float b1, float b2, float eps, float wd,
-                             int step, float grad_scale, hipStream_t s) {
-  if (nchunks <= 0) return 0;
+// computed here; no device sync).  Launches ceil(n / 16) kernels on `s`.
+KGWE_API int kgwe_adamw_step(const void* tensors, int n, float lr, float b1, float b2, float eps,
+                             float wd, int step, float grad_scale, hipStream_t s) {
+  if (n <= 0) return 0;
   AdamArgs a;
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
   a.bc1 = 1.f - powf(b1, static_cast<float>(step));
   a.bc2_sqrt_inv = 1.f / sqrtf(1.f - powf(b2, static_cast<float>(step)));
   a.grad_scale = grad_scale;
-  const int grid = nchunks < 4096 ? nchunks : 4096;
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, s,
-                     static_cast<const AdamTensor*>(tensors),
-                     static_cast<const AdamChunk*>(chunks), nchunks, a);
-  return KGWE_CHECK_LAUNCH();
+  const AdamTensor* ts = static_cast<const AdamTensor*>(tensors);
+  for (int base = 0; base < n; base += kBatch) {
+    AdamBatch b = {};
+    int64_t acc = 0;
+    for (int j = 0; j < kBatch && base + j < n; ++j) {
+      const AdamTensor& t = ts[base + j];
+      if (t.n <= 0 || t.p == nullptr || t.m == nullptr || t.v == nullptr || t.g == nullptr) return -1;
+      b.t[b.n] = t;
+      acc += (t.n + kChunk - 1) / kChunk;
+      b.chunk_end[b.n] = acc;
+      ++b.n;
+    }
+    const int grid = acc < 4096 ? static_cast<int>(acc) : 4096;
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, s, b, a);
+    const int rc = KGWE_CHECK_LAUNCH();
+    if (rc) return rc;
+  }
+  return 0;
 }

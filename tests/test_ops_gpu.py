@@ -217,3 +217,59 @@ def test_single_rank_train_step(parallel):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def test_fused_adamw_more_than_one_launch_batch():
+    """37 tensors -> three launches of <= 16 by-value pointer records."""
+    from kgwe.ops import FusedAdamW
+
+    torch.manual_seed(8)
+    shapes = [(17 * (i + 1) + (i % 3),) for i in range(37)] + [(70000,)]
+    ps = [torch.randn(s, device=DEV, requires_grad=True) for s in shapes]
+    pr = [p.detach().clone() for p in ps]
+    ms = [torch.zeros_like(p) for p in pr]
+    vs = [torch.zeros_like(p) for p in pr]
+    opt = FusedAdamW(ps, lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 3):
+        gs = [torch.randn_like(p) for p in ps]
+        for p, g in zip(ps, gs):
+            p.grad = g.clone()
+        opt.step()
+        for p, g, m, v in zip(pr, gs, ms, vs):
+            ref.adamw_(p, g, m, v, 1e-2, 0.9, 0.95, 1e-8, 0.1, step)
+    for p, r in zip(ps, pr):
+        assert torch.allclose(p.detach(), r, rtol=1e-5, atol=1e-6)
+
+
+def test_sharded_dp_overlapped_update_on_side_stream_matches_step_time_update():
+    """AdamW issued per bucket from backward hooks on a side HIP stream gives
+    the weights / optimizer state of the update run after backward.  Not
+    bit-exact: the RMSNorm weight gradient is accumulated with fp32 atomics,
+    so gradients differ in the last bits run to run; a race (weights read
+    while being updated, a missed wait) moves whole tensors by ~lr instead."""
+    from kgwe.models import llama
+    from kgwe.parallel.zero import ShardedDataParallel
+
+    tok = torch.randint(0, 1024, (2, 257), generator=torch.Generator().manual_seed(3)).to(DEV)
+    runs = []
+    for overlap in (True, False):
+        torch.manual_seed(5)
+        m = llama.build("tiny", device=DEV, dtype=torch.float32)
+        dp = ShardedDataParallel(m, lr=1e-3, bucket_elems=1 << 19, overlap_step=overlap)
+        assert len(dp.buckets) > 2
+        for _ in range(3):
+            loss = m(tok[:, :-1], tok[:, 1:])
+            loss.backward()
+            dp.step()
+        dp.wait_params()
+        torch.cuda.synchronize()
+        runs.append([(b.master.clone(), b.m.clone(), b.v.clone(), b.flat.clone())
+                     for b in dp.buckets])
+    lr = 1e-3
+    for i, (a, b) in enumerate(zip(*runs)):
+        d = (a[0] - b[0]).abs()  # fp32 master
+        assert d.mean().item() < 0.01 * lr, (i, d.mean().item())
+        assert (d > 0.5 * lr).float().mean().item() < 0.01, i
+        assert torch.allclose(a[1], b[1], rtol=1e-2, atol=1e-6)  # m
+        fd = (a[3].float() - b[3].float()).abs()  # bf16 weights
+        assert (fd > 0.5 * lr).float().mean().item() < 0.01, i

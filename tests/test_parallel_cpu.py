@@ -38,12 +38,12 @@ def _model():
     return llama.build("tiny", device="cpu", dtype=torch.float32)
 
 
-def _rank_main(rank, world, port, out, bucket_elems):
+def _rank_main(rank, world, port, out, bucket_elems, overlap=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         m = _model()
-        dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems)
+        dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems, overlap_step=overlap)
         losses = []
         for tok in _batches(world):
             mine = tok[rank:rank + 1]
@@ -62,7 +62,9 @@ def _rank_main(rank, world, port, out, bucket_elems):
 
 def _single_process_reference(world, bucket_elems):
     m = _model()
-    dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems)
+    # overlap off: the update runs in step(), after backward — the plain
+    # ordering the overlapped (in-hook) path must reproduce
+    dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems, overlap_step=False)
     assert dp.world == 1
     for tok in _batches(world):
         loss = m(tok[:, :-1], tok[:, 1:])  # mean over both ranks' tokens
@@ -101,10 +103,36 @@ def test_sharded_dp_world1_loss_decreases_and_weights_are_bucket_views():
         assert torch.equal(b.flat[:b.numel], b.master[:b.numel].to(torch.bfloat16))
 
 
+def test_sharded_dp_world1_overlapped_update_matches_step_time_update():
+    """The per-bucket AdamW issued from backward hooks gives bit-identical
+    weights and optimizer state to the update run after backward."""
+    tok = torch.randint(0, 1024, (2, 65), generator=torch.Generator().manual_seed(3))
+    runs = []
+    for overlap in (True, False):
+        m = _model()
+        dp = ShardedDataParallel(m, lr=LR, bucket_elems=1 << 20, overlap_step=overlap)
+        for _ in range(3):
+            loss = m(tok[:, :-1], tok[:, 1:])
+            loss.backward()
+            if overlap:  # every bucket was updated inside backward
+                assert all(b.updated for b in dp.buckets)
+                assert all(p.grad is None for p in m.parameters())
+            dp.step()
+        dp.wait_params()
+        runs.append((dp._step, [(b.master.clone(), b.m.clone(), b.v.clone(), b.flat.clone())
+                                for b in dp.buckets]))
+    assert runs[0][0] == runs[1][0] == 3
+    for a, b in zip(runs[0][1], runs[1][1]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("overlap", [True, False], ids=["overlap", "step-time"])
 @pytest.mark.parametrize("bucket_elems", [100 * 2**20, 1 << 20], ids=["one-bucket", "many-buckets"])
-def test_sharded_dp_world2_matches_single_process(tmp_path, bucket_elems):
+def test_sharded_dp_world2_matches_single_process(tmp_path, bucket_elems, overlap):
     world = 2
-    mp.spawn(_rank_main, args=(world, _port(), str(tmp_path), bucket_elems), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _port(), str(tmp_path), bucket_elems, overlap), nprocs=world,
+             join=True)
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
     if bucket_elems == 1 << 20:
