@@ -11,7 +11,8 @@ parameter count) — so this module is new, written MI355X-first:
 * fused gate|up (w13) projection -> one HIP SwiGLU kernel reading it in place;
 * residual add fused into RMSNorm (one HBM pass instead of two);
 * fused vocabulary cross-entropy (no fp32 logits copy);
-* GEMMs are plain hipBLASLt GEMMs via torch.nn.functional.linear.
+* GEMMs are hipBLASLt GEMMs; the weight-gradient GEMMs get their operands
+  transposed into the library's fast layouts (``K.linear``).
 """
 from __future__ import annotations
 
@@ -19,7 +20,6 @@ from dataclasses import asdict, dataclass
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops import attn as attn_ops
 from ..ops import functional as K
@@ -104,12 +104,12 @@ class Attention(nn.Module):
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
         B, S, _ = x.shape
         c = self.cfg
-        qkv = F.linear(x, self.wqkv).view(B * S, -1)
+        qkv = K.linear(x, self.wqkv).view(B * S, -1)
         q, k, v = K.rope_qkv(qkv, cos, sin, S, c.n_heads, c.n_kv_heads, c.head_dim)
         o = attn_ops.attention(q.view(B, S, c.n_heads, c.head_dim),
                                k.view(B, S, c.n_kv_heads, c.head_dim),
                                v.view(B, S, c.n_kv_heads, c.head_dim), causal=True)
-        return F.linear(o.reshape(B, S, -1), self.wo)
+        return K.linear(o.reshape(B, S, -1), self.wo)
 
 
 class FeedForward(nn.Module):
@@ -119,7 +119,7 @@ class FeedForward(nn.Module):
         self.w2 = nn.Parameter(torch.empty(cfg.dim, cfg.ffn_dim))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return F.linear(K.swiglu(F.linear(x, self.w13)), self.w2)
+        return K.linear(K.swiglu(K.linear(x, self.w13)), self.w2)
 
 
 class TransformerBlock(nn.Module):
@@ -181,7 +181,7 @@ class Llama(nn.Module):
 
     def forward(self, tokens: torch.Tensor, labels: torch.Tensor | None = None):
         h = self.forward_hidden(tokens)
-        logits = F.linear(h, self.output)
+        logits = K.linear(h, self.output)
         if labels is None:
             return logits
         return K.cross_entropy(logits, labels)

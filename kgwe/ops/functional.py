@@ -209,3 +209,57 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
         return _CrossEntropy.apply(logits.contiguous(), labels.to(torch.int64).contiguous(),
                                    ignore_index)
     return ref.cross_entropy(logits, labels, ignore_index)
+
+
+# --------------------------------------------------------------------------
+# Linear layer with layout-aware weight-gradient GEMMs
+# --------------------------------------------------------------------------
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """[R, C] bf16 -> contiguous [C, R] (LDS-tiled HIP transpose)."""
+    _require(x.dim() == 2 and x.dtype == torch.bfloat16 and x.is_contiguous()
+             and x.shape[0] % 8 == 0 and x.shape[1] % 8 == 0,
+             "transpose: contiguous bf16 [R, C] with R % 8 == 0 and C % 8 == 0")
+    out = torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=x.dtype)
+    check(lib().kgwe_transpose_bf16(ptr(x), ptr(out), x.shape[0], x.shape[1], stream(x)),
+          "transpose_bf16")
+    return out
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T.  Forward and input gradient are the plain library GEMMs;
+    the weight gradient dW = dY^T X — a reduction over the leading (token)
+    dimension of both stored operands, the slowest hipBLASLt layout on MI355X
+    — is issued after transposing the SMALLER of X / dY, which moves it to
+    the "tt" / "nn" kernels (tools/gemm_layouts.py: ~1.35 vs ~1.1 PF/s for
+    the Llama-3-8B shapes; the transpose of a [T, 4096] operand costs ~25 us)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return torch.nn.functional.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        N, K = w.shape
+        x2 = x.reshape(-1, K)
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            if x2.shape[0] % 8 or N % 8 or K % 8 or not x2.is_contiguous():
+                dw = torch.mm(dy2.t(), x2)
+            elif N >= K:
+                dw = torch.mm(dy2.t(), transpose(x2).t())   # "tt"
+            else:
+                dw = torch.mm(transpose(dy2), x2)           # "nn"
+        return dx, dw
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if use_hip(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+        return _Linear.apply(x, w)
+    return torch.nn.functional.linear(x, w)

@@ -273,3 +273,28 @@ def test_sharded_dp_overlapped_update_on_side_stream_matches_step_time_update():
         assert torch.allclose(a[1], b[1], rtol=1e-2, atol=1e-6)  # m
         fd = (a[3].float() - b[3].float()).abs()  # bf16 weights
         assert (fd > 0.5 * lr).float().mean().item() < 0.01, i
+
+
+@pytest.mark.parametrize("shape", [(8192, 4096), (136, 72), (64, 8)])
+def test_transpose_bf16(shape):
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    assert torch.equal(K.transpose(x), x.t().contiguous())
+
+
+@pytest.mark.parametrize("N,Kd", [(6144, 512), (512, 1536), (1000, 64)])
+def test_linear_layout_aware_backward_matches_fp32(N, Kd):
+    """Weight gradient through the transposed-operand GEMMs ("tt" for N >= K,
+    "nn" otherwise; odd sizes fall back to the plain layout) vs fp32."""
+    torch.manual_seed(9)
+    x = torch.randn(2, 256, Kd, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, Kd, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_()
+    y = K.linear(x, w)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    yf = xf @ wf.t()
+    yf.backward(g.float())
+    assert torch.allclose(y.float(), yf, rtol=2e-2, atol=2e-2)
+    for got, want in ((x.grad, xf.grad), (w.grad, wf.grad)):
+        err = (got.float() - want).abs().max().item()
+        assert err <= 2e-2 * want.abs().max().item() + 1e-2, err
