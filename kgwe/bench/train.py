@@ -27,7 +27,7 @@ from ..utils.amdsmi_util import UtilSampler
 class TrainConfig:
     model: str = "llama3-8b"
     seq_len: int = 4096
-    micro_batch: int = 2
+    micro_batch: int = 4
     lr: float = 3e-4
     activation_checkpointing: bool = False
     # "zero": replicated bf16 weights + sharded fp32 optimizer state with

@@ -9,8 +9,8 @@
 //         y = h * rstd * w
 //   bwd:  g  = dy * w
 //         dx = rstd * (g - h * rstd^2 * mean(g * h)) (+ dadd)
-//         dw = sum_rows(dy * h * rstd)   — per-wave fp32 sums in LDS, reduced
-//              per workgroup, then fp32 atomics into one [H] accumulator.
+//         dw = sum_rows(dy * h * rstd)   — per-lane fp32 sums in registers,
+//              reduced per workgroup, then fp32 atomics into one [H] accumulator.
 //
 // Used by every Llama block (attention_norm / ffn_norm / final norm); fusing
 // the residual add saves one full HBM round-trip of the hidden state.
@@ -68,66 +68,69 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   }
 }
 
-// Grid: G workgroups of 4 waves; waves stride over rows.  Each workgroup adds
-// its dw contribution into the fp32 accumulator `partial[H]`.
+// Grid: G workgroups of 4 waves; workgroups stride over rows, and the 4
+// waves of a workgroup split each row's columns (wave w owns the NV/4 16-B
+// vectors w, w+4, ... of every lane-slot), so a lane holds only NV/4 vectors
+// of dy and of h (cached in registers: each byte is read from HBM once) and
+// 2*NV fp32 dw partial sums — few enough registers for 8 waves per SIMD,
+// which is what hides HBM latency in this kernel.  The row's dot product is
+// combined across the 4 waves through a double-buffered LDS word per wave
+// (one barrier per row).  At the end each workgroup adds its dw partial sums
+// with one no-return fp32 atomic per column into partial[H] (G x H x 4 B).
 template <int NV>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
     const bf16_t* __restrict__ w, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ dadd, bf16_t* __restrict__ dx,
     float* __restrict__ partial, int T, int H) {
-  // [4][H] fp32: each wave accumulates its rows' dw contribution in its own
-  // LDS row (lane-private columns, so no intra-wave sync), keeping VGPRs for
-  // the two cached input rows (dy, h).
-  extern __shared__ float lds[];
+  constexpr int NW = NV >= 4 ? NV / 4 : 1;  // vectors per lane per row
+  __shared__ float dots[2][4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int nwaves = gridDim.x * 4;
-  float* acc = lds + wid * H;
+  const bool active = NV >= 4 || wid < NV;  // H = 512 / 1024: fewer vectors than waves
+  float dw[NW][8];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    f32x4* a = reinterpret_cast<f32x4*>(acc + (i * kWave + lane) * 8);
-    a[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    a[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int i = 0; i < NW; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw[i][j] = 0.f;
   const float invH = 1.f / static_cast<float>(H);
-  for (int row = blockIdx.x * 4 + wid; row < T; row += nwaves) {
+  int parity = 0;
+  for (int row = blockIdx.x; row < T; row += gridDim.x, parity ^= 1) {
     const size_t base = static_cast<size_t>(row) * H;
     const float rstd = rstd_in[row];
-    // Pass 1: dot = sum(dy*w*h) and the dw contribution.  Pass 2 re-reads the
-    // row (L2-hot: 16 KB per wave just touched) instead of caching it in
-    // VGPRs, which keeps the kernel at high occupancy for any H.
+    bf16x8 d[NW], hv[NW];
     float dot = 0.f;
-#pragma unroll 4
-    for (int i = 0; i < NV; ++i) {
-      const int col = (i * kWave + lane) * 8;
-      const bf16x8 d = *reinterpret_cast<const bf16x8*>(dy + base + col);
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + base + col);
-      const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + col);
-      f32x4* a = reinterpret_cast<f32x4*>(acc + col);
-      f32x4 a0 = a[0], a1 = a[1];
+    if (active) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        a0[j] += bf2f(d[j]) * bf2f(hv[j]) * rstd;
-        a1[j] += bf2f(d[j + 4]) * bf2f(hv[j + 4]) * rstd;
+      for (int i = 0; i < NW; ++i) {
+        const int col = ((i * 4 + wid) * kWave + lane) * 8;
+        d[i] = *reinterpret_cast<const bf16x8*>(dy + base + col);
+        hv[i] = *reinterpret_cast<const bf16x8*>(h + base + col);
       }
-      a[0] = a0;
-      a[1] = a1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dot += bf2f(d[j]) * bf2f(wv[j]) * bf2f(hv[j]);
+      for (int i = 0; i < NW; ++i) {
+        const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + ((i * 4 + wid) * kWave + lane) * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dot += bf2f(d[i][j]) * bf2f(wv[j]) * bf2f(hv[i][j]);
+      }
+      dot = wave_sum(dot);
     }
-    dot = wave_sum(dot) * invH;
+    if (lane == 0) dots[parity][wid] = dot;
+    __syncthreads();  // the other parity slot is rewritten only after the next barrier
+    dot = (dots[parity][0] + dots[parity][1] + dots[parity][2] + dots[parity][3]) * invH;
+    if (!active) continue;
     const float c = rstd * rstd * dot;
-#pragma unroll 4
-    for (int i = 0; i < NV; ++i) {
-      const int col = (i * kWave + lane) * 8;
-      const bf16x8 d = *reinterpret_cast<const bf16x8*>(dy + base + col);
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(h + base + col);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int col = ((i * 4 + wid) * kWave + lane) * 8;
       const bf16x8 wv = *reinterpret_cast<const bf16x8*>(w + col);
       float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        o[j] = rstd * (bf2f(d[j]) * bf2f(wv[j]) - bf2f(hv[j]) * c);
+      for (int j = 0; j < 8; ++j) {
+        const float df = bf2f(d[i][j]), hf = bf2f(hv[i][j]);
+        dw[i][j] += df * hf * rstd;
+        o[j] = rstd * (df * bf2f(wv[j]) - hf * c);
+      }
       if (dadd) {
         float a[8];
         load8(dadd + base + col, a);
@@ -137,18 +140,20 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
       store8(dx + base + col, o);
     }
   }
-  __syncthreads();
-  // Reduce the 4 waves' rows in LDS, then one no-return fp32 atomic per
-  // column per workgroup into dw_acc[H] (zeroed by the launcher): G x H adds
-  // of 4 B = ~8 MB at the ~1.3 TB/s chip atomic rate, instead of a serial
-  // column-sum pass over a [G, H] partial buffer.
-  for (int c4 = threadIdx.x; c4 < H / 4; c4 += 256) {
-    f32x4 s = reinterpret_cast<f32x4*>(lds)[c4];
+  // Stage the workgroup's dw row in LDS, then add it with atomics whose 64
+  // lanes cover 256 contiguous bytes (the full-rate atomic shape; lanes 32 B
+  // apart run ~8x slower: MI355X_MICROARCH.md, global float atomics).
+  extern __shared__ float red[];  // H floats
+  if (active) {
 #pragma unroll
-    for (int k = 1; k < 4; ++k) s += reinterpret_cast<f32x4*>(lds + k * H)[c4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) atomicAdd(partial + c4 * 4 + j, s[j]);
+    for (int i = 0; i < NW; ++i) {
+      f32x4* r = reinterpret_cast<f32x4*>(red + ((i * 4 + wid) * kWave + lane) * 8);
+      r[0] = f32x4{dw[i][0], dw[i][1], dw[i][2], dw[i][3]};
+      r[1] = f32x4{dw[i][4], dw[i][5], dw[i][6], dw[i][7]};
+    }
   }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256) atomicAdd(partial + c, red[c]);
 }
 
 // dw = dw_acc cast to the parameter dtype.
@@ -175,9 +180,8 @@ template <int NV>
 int launch_bwd(const bf16_t* dy, const bf16_t* h, const bf16_t* w,
                const float* rstd, const bf16_t* dadd, bf16_t* dx,
                float* partial, int G, int T, int H, hipStream_t s) {
-  hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(G), dim3(256),
-                     4 * H * sizeof(float), s, dy, h, w, rstd, dadd, dx,
-                     partial, T, H);
+  hipLaunchKernelGGL(rmsnorm_bwd_kernel<NV>, dim3(G), dim3(256), H * sizeof(float), s, dy, h, w,
+                     rstd, dadd, dx, partial, T, H);
   return KGWE_CHECK_LAUNCH();
 }
 
@@ -186,8 +190,7 @@ int launch_bwd(const bf16_t* dy, const bf16_t* h, const bf16_t* w,
 // Workgroups of the backward (rows are strided over them); the caller's
 // `partial` buffer only needs H floats (fp32 dw accumulator).
 KGWE_API int kgwe_rmsnorm_bwd_grid(int T) {
-  int g = (T + 3) / 4;
-  return g < 512 ? (g < 1 ? 1 : g) : 512;
+  return T < 1024 ? (T < 1 ? 1 : T) : 1024;  // 4 workgroups (16 waves) per CU
 }
 
 // Returns 0 on success, -1 for an unsupported H (must be 512 * {1,2,4,8,16}).
