@@ -214,20 +214,29 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
 # --------------------------------------------------------------------------
 # Linear layer with layout-aware weight-gradient GEMMs
 # --------------------------------------------------------------------------
-def transpose(x: torch.Tensor) -> torch.Tensor:
-    """[R, C] bf16 -> contiguous [C, R] (LDS-tiled HIP transpose)."""
+def transpose(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """[R, C] bf16 -> contiguous [C, R] (LDS-tiled HIP transpose; fp32-free
+    copy on CPU)."""
+    if not use_hip(x):
+        t = x.t().contiguous()
+        return t if out is None else out.copy_(t)
     _require(x.dim() == 2 and x.dtype == torch.bfloat16 and x.is_contiguous()
              and x.shape[0] % 8 == 0 and x.shape[1] % 8 == 0,
              "transpose: contiguous bf16 [R, C] with R % 8 == 0 and C % 8 == 0")
-    out = torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=x.dtype)
+    if out is None:
+        out = torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=x.dtype)
+    _require(out.shape == (x.shape[1], x.shape[0]) and out.dtype == x.dtype and out.is_contiguous()
+             and out.device == x.device, "transpose: out must be a contiguous [C, R] bf16 tensor")
     check(lib().kgwe_transpose_bf16(ptr(x), ptr(out), x.shape[0], x.shape[1], stream(x)),
           "transpose_bf16")
     return out
 
 
 class _Linear(torch.autograd.Function):
-    """y = x W^T.  Forward and input gradient are the plain library GEMMs;
-    the weight gradient dW = dY^T X — a reduction over the leading (token)
+    """y = x W^T.  Forward is the plain library GEMM ("nt"); the input
+    gradient uses the weight's persistent transposed copy when one exists
+    (``w._kgwe_wt``, kept by kgwe.parallel.zero) so it runs "nt" as well; the
+    weight gradient dW = dY^T X — a reduction over the leading (token)
     dimension of both stored operands, the slowest hipBLASLt layout on MI355X
     — is issued after transposing the SMALLER of X / dY, which moves it to
     the "tt" / "nn" kernels (tools/gemm_layouts.py: ~1.35 vs ~1.1 PF/s for
@@ -236,6 +245,9 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         ctx.save_for_backward(x, w)
+        # Persistent W^T copy kept by the data-parallel wrapper, if any
+        # (kgwe.parallel.zero): makes dX = dY W an "nt" GEMM.
+        ctx.wt = getattr(w, "_kgwe_wt", None)
         return torch.nn.functional.linear(x, w)
 
     @staticmethod
@@ -248,7 +260,8 @@ class _Linear(torch.autograd.Function):
             dy2 = dy2.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(x.shape)
+            wt = ctx.wt
+            dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(x.shape)
         if ctx.needs_input_grad[1]:
             if x2.shape[0] % 8 or N % 8 or K % 8 or not x2.is_contiguous():
                 dw = torch.mm(dy2.t(), x2)

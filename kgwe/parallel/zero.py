@@ -44,12 +44,14 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from ..ops import functional as K
 from ..ops.adamw import AdamPlan
 
 
 class _Bucket:
     __slots__ = ("params", "offsets", "numel", "padded", "shard", "flat", "master", "m", "v",
-                 "gfull", "gshard", "pending", "seen", "rs_work", "ag_work", "ready", "updated")
+                 "gfull", "gshard", "pending", "seen", "rs_work", "ag_work", "ready", "updated",
+                 "tparams", "flat_t")
 
 
 class ShardedDataParallel:
@@ -64,11 +66,21 @@ class ShardedDataParallel:
     a weight (dX = dY W) runs in the same autograd node that produces that
     weight's gradient, before the accumulate-grad hook fires.  This assumes
     each parameter receives ONE gradient per backward (no weight tying).
-    The next forward waits per bucket in a module pre-hook."""
+    The next forward waits per bucket in a module pre-hook.
+
+    transposed_weights=True (GPU): every linear weight W [N, K] also keeps a
+    bf16 copy of W^T [K, N] (``p._kgwe_wt``), refreshed on the side stream
+    right after the bucket's update (world 1) or all-gather (world N).  The
+    input-gradient GEMM dX = dY W then runs as dY (W^T)^T — hipBLASLt's "nt"
+    layout, ~1.5 PF/s on MI355X against ~1.35 for the "nn" layout W needs
+    (tools/gemm_layouts.py) — at the price of 2 B/param of HBM (15 GB for an
+    8B model, of 288 GB) and one 2x16 GB transpose pass per step, overlapped
+    with backward."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, bucket_elems: int = 100 * 2**20,
-                 reduce_dtype: torch.dtype = torch.float32, group=None, overlap_step: bool = True):
+                 reduce_dtype: torch.dtype = torch.float32, group=None, overlap_step: bool = True,
+                 transposed_weights: bool = True):
         self.model = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.group = group
@@ -95,6 +107,7 @@ class ShardedDataParallel:
             cur.append(p)
             n += p.numel()
         self.buckets.append(self._make_bucket(cur))
+        self._setup_transposed(model, transposed_weights and self.device.type == "cuda")
         self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
         self._slot = {id(p): (b, o) for b in self.buckets for p, o in zip(b.params, b.offsets)}
         self._hooks = []
@@ -148,6 +161,30 @@ class ShardedDataParallel:
         b.updated = False
         return b
 
+    def _setup_transposed(self, model, enabled: bool) -> None:
+        embed = {id(m.weight) for m in model.modules() if isinstance(m, torch.nn.Embedding)}
+        for b in self.buckets:
+            b.tparams = []
+            b.flat_t = None
+            if not enabled:
+                continue
+            b.tparams = [p for p in b.params if p.dim() == 2 and id(p) not in embed
+                         and p.shape[0] % 8 == 0 and p.shape[1] % 8 == 0]
+            n = sum(p.numel() for p in b.tparams)
+            if n == 0:
+                continue
+            b.flat_t = torch.empty(n, dtype=torch.bfloat16, device=self.device)
+            off = 0
+            for p in b.tparams:
+                p._kgwe_wt = b.flat_t[off:off + p.numel()].view(p.shape[1], p.shape[0])
+                off += p.numel()
+            self._refresh_transposed(b)
+
+    def _refresh_transposed(self, b: _Bucket) -> None:
+        """W^T copies of bucket b's linear weights, on the current stream."""
+        for p in b.tparams:
+            K.transpose(p.detach(), out=p._kgwe_wt)
+
     # ------------------------------------------------------------ backward
     @torch.no_grad()
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
@@ -195,6 +232,12 @@ class ShardedDataParallel:
                                   grad_scale=1.0 / self.world)
                 b.ag_work = dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard],
                                                         group=self.group, async_op=True)
+                if b.tparams and side is not None:
+                    b.ag_work.wait()  # the side stream waits for the gathered weights
+                    b.ag_work = None
+                    self._refresh_transposed(b)
+                    b.ready = torch.cuda.Event()
+                    b.ready.record(side)
             else:
                 entries = []
                 for p, o in zip(b.params, b.offsets):
@@ -209,6 +252,7 @@ class ShardedDataParallel:
                                     b.flat[o:o + n]))
                     p.grad = None
                 self._plan.launch(entries, self.lr, b1, b2, self.eps, self.wd, self._step)
+                self._refresh_transposed(b)
                 if side is not None:
                     b.ready = torch.cuda.Event()
                     b.ready.record(side)
@@ -280,3 +324,5 @@ class ShardedDataParallel:
                 b.ag_work = dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard],
                                                         group=self.group, async_op=True)
         self.wait_params()
+        for b in self.buckets:
+            self._refresh_transposed(b)

@@ -263,6 +263,11 @@ def test_sharded_dp_overlapped_update_on_side_stream_matches_step_time_update():
             dp.step()
         dp.wait_params()
         torch.cuda.synchronize()
+        # the persistent W^T copies (dgrad "nt" layout) track the updated weights
+        assert sum(len(b.tparams) for b in dp.buckets) == 1 + 4 * 2  # output + 4 per block
+        for b in dp.buckets:
+            for p in b.tparams:
+                assert torch.equal(p._kgwe_wt, p.detach().t()), p.shape
         runs.append([(b.master.clone(), b.m.clone(), b.v.clone(), b.flat.clone())
                      for b in dp.buckets])
     lr = 1e-3
