@@ -1,0 +1,93 @@
+"""The world > 1 sharded-DP path with its HIP streams, on ONE MI355X.
+
+RCCL refuses two ranks on one GPU, so this runs the gloo backend with both
+ranks' tensors on cuda:0: the same hooks, side-stream AdamW, per-bucket
+reduce-scatter / all-gather (gloo's CUDA work is ordered against the
+issuing stream like RCCL's), transposed weight copies and forward waits as
+the 8-GPU RCCL run — checked against one process that sees both ranks'
+batches.  Two ranks only (box limit: 16 GPU processes).
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 3
+LR = 1e-3
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batches():
+    g = torch.Generator().manual_seed(11)
+    return [torch.randint(0, 1024, (2, 257), generator=g) for _ in range(STEPS)]
+
+
+def _model():
+    from kgwe.models import llama
+
+    torch.manual_seed(0)
+    return llama.build("tiny", device="cuda:0", dtype=torch.float32)
+
+
+def _rank_main(rank, world, port, out):
+    from kgwe.parallel.zero import ShardedDataParallel
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = _model()
+        dp = ShardedDataParallel(m, lr=LR, bucket_elems=1 << 19)
+        for tok in _batches():
+            mine = tok[rank:rank + 1].cuda()
+            loss = m(mine[:, :-1], mine[:, 1:])
+            loss.backward()
+            dp.step()
+        dp.wait_params()
+        torch.cuda.synchronize()
+        for b in dp.buckets:
+            for p in b.tparams:
+                assert torch.equal(p._kgwe_wt, p.detach().t())
+        torch.save({"flat": [b.flat.cpu() for b in dp.buckets],
+                    "master": [b.master.cpu() for b in dp.buckets],
+                    "numel": [b.numel for b in dp.buckets]}, f"{out}/rank{rank}.pt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_dp_two_ranks_on_one_gpu_matches_single_process(tmp_path):
+    if not dist.is_gloo_available():
+        pytest.skip("gloo backend not built")
+    mp.spawn(_rank_main, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for a, b in zip(r0["flat"], r1["flat"]):  # replicas identical after the all-gathers
+        assert torch.equal(a, b)
+    from kgwe.parallel.zero import ShardedDataParallel
+
+    m = _model()
+    dp = ShardedDataParallel(m, lr=LR, bucket_elems=1 << 19, overlap_step=False)
+    for tok in _batches():
+        t = tok.cuda()
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        dp.step()
+    dp.wait_params()
+    for i, b in enumerate(dp.buckets):
+        got = torch.cat([r0["master"][i], r1["master"][i]])[:b.numel]
+        want = b.master[:b.numel].cpu()
+        d = (got - want).abs()
+        assert d.mean().item() < 0.02 * LR * STEPS, (i, d.mean().item())
+        assert (d > 0.5 * LR).float().mean().item() < 0.01, i
