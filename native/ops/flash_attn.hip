@@ -62,6 +62,12 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// 2^x as ONE v_exp_f32.  exp2f() adds a denormal-range fixup around it
+// (v_cmp + v_cndmask + v_add before, v_ldexp after: 4 extra VALU per element,
+// ~30 % of the softmax VALU stream); softmax arguments are <= 0 and a result
+// below 2^-126 is 0 to within bf16 anyway.  exp(-inf) is still 0.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ bf16x8 cat44(u16x4 lo, u16x4 hi) {
   bf16x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
@@ -114,6 +120,7 @@ constexpr int VTILE = BKV * HD;     // bf16 elements of one V buffer
 // 64 keys double-buffered in LDS (67 KB): the global loads of tile t+1 are
 // issued before tile t's MFMAs and written to the other buffer after them, so
 // one barrier per tile separates the phases.
+template <bool EVEN>
 __global__ __launch_bounds__(512) void fa_fwd_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, float* __restrict__ lse2, int S, int Hq, int Hkv, float c,
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
   {
     const bf16_t* qp = q + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) qf[t] = qrow < S ? ld16(qp + 16 * t + 8 * hh) : bf16x8{};
+    for (int t = 0; t < 8; ++t) qf[t] = (EVEN || qrow < S) ? ld16(qp + 16 * t + 8 * hh) : bf16x8{};
   }
   f32x16 oacc[4];
 #pragma unroll
@@ -153,7 +160,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = kt * BKV + skey + 32 * i;
-      if (s < S) {
+      if (EVEN || s < S) {
         kr[i] = ld16(kb + static_cast<size_t>(s) * kvs + sch * 8);
         vr[i] = ld16(vb + static_cast<size_t>(s) * kvs + sch * 8);
       } else {
@@ -194,7 +201,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
         for (int t = 0; t < 8; ++t)
           sacc[st] = mfma(ld16(&Kc[(st * 32 + lq) * KST + 16 * t + 8 * hh]), qf[t], sacc[st]);
       float mx = -INFINITY;
-      const bool edge = (causal && k0 + BKV - 1 > q0) || k0 + BKV > S;  // wave-uniform
+      const bool edge = (causal && k0 + BKV - 1 > q0) || (!EVEN && k0 + BKV > S);  // wave-uniform
       if (edge) {
 #pragma unroll
         for (int st = 0; st < 2; ++st)
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + st * 32 + acc_row(r, hh);
             float s = sacc[st][r] * c;
-            if (key >= S || (causal && key > qrow)) s = -INFINITY;
+            if ((!EVEN && key >= S) || (causal && key > qrow)) s = -INFINITY;
             sacc[st][r] = s;
             mx = fmaxf(mx, s);
           }
@@ -221,7 +228,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
       // Rescale O only when some row's max moved (exact; after the first few
       // tiles the running max rarely changes).
       if (__any(m_new > m)) {
-        const float alpha = exp2f(m - m_use);
+        const float alpha = fast_exp2(m - m_use);
         l *= alpha;
 #pragma unroll
         for (int db = 0; db < 4; ++db)
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(sacc[st][r] - m_use);
+          const float p = fast_exp2(sacc[st][r] - m_use);
           sacc[st][r] = p;
           rs += p;
         }
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
     if (kt + 1 < ntiles) swrite(cur ^ 1);  // the buffer every wave finished last tile
     __syncthreads();
   }
-  if (qrow < S) {
+  if (EVEN || qrow < S) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16_t* op = o + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
@@ -340,6 +347,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* img, int base, int db, i
 // Register budget: <= 256 per lane so two workgroups share a CU (2 waves per
 // SIMD) — over it, hipcc parks the excess in AGPRs and moves it back and forth
 // every iteration.  K stays in VGPRs, the WG's V tile is read from LDS.
+template <bool EVEN>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
@@ -365,13 +373,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   {
     const size_t off = (static_cast<size_t>(b) * S + key) * kvs + static_cast<size_t>(hkv) * HD;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) kf[t] = key < S ? ld16(k + off + 16 * t + 8 * hh) : bf16x8{};
+    for (int t = 0; t < 8; ++t) kf[t] = (EVEN || key < S) ? ld16(k + off + 16 * t + 8 * hh) : bf16x8{};
     // V rows kb*128 .. +127 -> layout-(b) image (row reads only); published
     // by the barrier before the main loop.
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = (threadIdx.x >> 4) + 16 * i, ch = threadIdx.x & 15, s = kb * 128 + r;
-      const bf16x8 x = s < S ? ld16(v + (static_cast<size_t>(b) * S + s) * kvs +
+      const bf16x8 x = (EVEN || s < S) ? ld16(v + (static_cast<size_t>(b) * S + s) * kvs +
                                     static_cast<size_t>(hkv) * HD + ch * 8)
                              : bf16x8{};
       *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Vw) + a_off(r, ch)) = x;
@@ -389,21 +397,22 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   const int sr = threadIdx.x >> 4, sch = threadIdx.x & 15;
   bf16x8 qr[2], dr[2];
   float lr = 0.f, drl = 0.f;
-  auto gload = [&](int it) {
-    const int g = it % G, qt = nqt - 1 - it / G;
+  // Iteration it = (query tile nqt-1 - it/G, head g = it%G), tracked
+  // incrementally (G is a runtime value: no per-iteration integer division).
+  auto gload = [&](int g, int qt) {
     const int h = hkv * G + g;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int s = qt * BQT + sr + 16 * i;
       const size_t off = (static_cast<size_t>(b) * S + s) * qs + static_cast<size_t>(h) * HD + sch * 8;
-      qr[i] = s < S ? ld16(q + off) : bf16x8{};
-      dr[i] = s < S ? ld16(dout + off) : bf16x8{};
+      qr[i] = (EVEN || s < S) ? ld16(q + off) : bf16x8{};
+      dr[i] = (EVEN || s < S) ? ld16(dout + off) : bf16x8{};
     }
     if (threadIdx.x < BQT) {
       const int s = qt * BQT + threadIdx.x;
       const size_t li = (static_cast<size_t>(b) * Hq + h) * S + s;
-      lr = s < S ? lse2[li] : INFINITY;
-      drl = s < S ? delta[li] : 0.f;
+      lr = (EVEN || s < S) ? lse2[li] : INFINITY;
+      drl = (EVEN || s < S) ? delta[li] : 0.f;
     }
   };
   auto swrite = [&](int buf) {
@@ -421,9 +430,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
   const int tr_row = 4 * (trG >> 1) + trq, tr_ch = 2 * (trG & 1) + (trp >> 1), tr_byte = 8 * (trp & 1);
   if (total > 0) {
-    gload(0);
+    gload(0, nqt - 1);
     swrite(0);
   }
+  int qt = nqt - 1, g_cur = 0;
   __syncthreads();
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
@@ -431,8 +441,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     // a (batch, kv head) — all resident on one XCD — reads the same Q / dO
     // tile at the same time (one L2 fill, not one per key block); a block
     // stops when the sweep passes its diagonal.
-    const int qt = nqt - 1 - it / G;
-    if (it + 1 < total) gload(it + 1);
+    const int g_nxt = g_cur + 1 == G ? 0 : g_cur + 1;
+    const int qt_nxt = g_nxt == 0 ? qt - 1 : qt;
+    if (it + 1 < total) gload(g_nxt, qt_nxt);
     const int qbase = qt * BQT;
     if (!causal || qbase + BQT - 1 >= key0) {  // else every query of this tile precedes our keys
       const bf16_t* Qc = Qs + cur * QTILE;
@@ -447,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
         pa = mfma(row_read(Dc, lk, 2 * t + hh), row_read(Vmine, lk, 2 * t + hh), pa);
       }
       // P = exp2(S c - lse2), dS = P (dP - delta); row r <-> query qbase + acc_row(r).
-      const bool edge = (causal && key0 + 31 > qbase) || qbase + BQT > S || key0 + 32 > S;
+      const bool edge = (causal && key0 + 31 > qbase) || (!EVEN && (qbase + BQT > S || key0 + 32 > S));
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         // accumulator rows 4*g4 .. +3 are queries 8*g4 + 4*hh + 0..3: one b128 read each
@@ -456,10 +467,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g4 + j;
-          float p = exp2f(sa[r] * c - lse4[j]);
+          float p = fast_exp2(sa[r] * c - lse4[j]);
           if (edge) {
             const int qrow = qbase + acc_row(r, hh);
-            if (key >= S || qrow >= S || (causal && key > qrow)) p = 0.f;
+            if ((!EVEN && (key >= S || qrow >= S)) || (causal && key > qrow)) p = 0.f;
           }
           sa[r] = p;
           pa[r] = p * (pa[r] - del4[j]);
@@ -483,8 +494,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     }
     if (it + 1 < total) swrite(cur ^ 1);
     __syncthreads();
+    qt = qt_nxt;
+    g_cur = g_nxt;
   }
-  if (key < S) {
+  if (EVEN || key < S) {
     const size_t off = (static_cast<size_t>(b) * S + key) * kvs + static_cast<size_t>(hkv) * HD;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
@@ -506,6 +519,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
 // forward's geometry: query on the lane).  K and V tiles double-buffered in
 // layout-(b) images: K rows for S^T = K Q^T and K columns (transposed reads)
 // for dQ^T += K^T dS^T from the same image; V rows for dP^T = V dO^T.
+template <bool EVEN>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
@@ -525,13 +539,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const size_t off = (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      qf[t] = qrow < S ? ld16(q + off + 16 * t + 8 * hh) : bf16x8{};
-      df[t] = qrow < S ? ld16(dout + off + 16 * t + 8 * hh) : bf16x8{};
+      qf[t] = (EVEN || qrow < S) ? ld16(q + off + 16 * t + 8 * hh) : bf16x8{};
+      df[t] = (EVEN || qrow < S) ? ld16(dout + off + 16 * t + 8 * hh) : bf16x8{};
     }
   }
   const size_t li = (static_cast<size_t>(b) * Hq + h) * S + qrow;
-  const float my_lse = qrow < S ? lse2[li] : INFINITY;
-  const float my_delta = qrow < S ? delta[li] : 0.f;
+  const float my_lse = (EVEN || qrow < S) ? lse2[li] : INFINITY;
+  const float my_delta = (EVEN || qrow < S) ? delta[li] : 0.f;
   f32x16 dqa[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) dqa[i] = f32x16{};
@@ -546,8 +560,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = kt * BKV + skey + 16 * i;
-      kr[i] = s < S ? ld16(kb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
-      vr[i] = s < S ? ld16(vb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
+      kr[i] = (EVEN || s < S) ? ld16(kb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
+      vr[i] = (EVEN || s < S) ? ld16(vb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
     }
   };
   auto swrite = [&](int buf) {
@@ -570,7 +584,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     if (!causal || k0 <= q0 + 31) {
       const bf16_t* Kc = Ks + cur * VTILE;
       const bf16_t* Vc = Vs + cur * VTILE;
-      const bool edge = (causal && k0 + BKV - 1 > q0) || k0 + BKV > S || q0 + 32 > S;
+      const bool edge = (causal && k0 + BKV - 1 > q0) || (!EVEN && (k0 + BKV > S || q0 + 32 > S));
       // Two 32-key halves in sequence: one S^T / dP^T accumulator pair live
       // at a time keeps the kernel inside 256 VGPRs.
 #pragma unroll
@@ -583,10 +597,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(sa[r] * c - my_lse);
+          float p = fast_exp2(sa[r] * c - my_lse);
           if (edge) {
             const int kk = k0 + st * 32 + acc_row(r, hh);
-            if (kk >= S || qrow >= S || (causal && kk > qrow)) p = 0.f;
+            if ((!EVEN && (kk >= S || qrow >= S)) || (causal && kk > qrow)) p = 0.f;
           }
           pa[r] = p * (pa[r] - my_delta);  // dS^T
         }
@@ -605,7 +619,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     if (kt + 1 < ntiles) swrite(cur ^ 1);
     __syncthreads();
   }
-  if (qrow < S) {
+  if (EVEN || qrow < S) {
     bf16_t* p = dq + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
@@ -638,17 +652,29 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
   int rc = KGWE_CHECK_LAUNCH();
   if (rc) return rc;
   const int nKB = (S + 127) / 128;
-  hipLaunchKernelGGL(fa_bwd_dkdv_kernel, dim3(static_cast<unsigned>(B * Hkv * nKB)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
-                     static_cast<const bf16_t*>(v), static_cast<const bf16_t*>(dout), lse2, work,
-                     static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv), S, Hq, Hkv, c, scale, causal, nKB);
-  rc = KGWE_CHECK_LAUNCH();
-  if (rc) return rc;
   const int nQB = (S + BQ - 1) / BQ;
-  hipLaunchKernelGGL(fa_bwd_dq_kernel, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
-                     static_cast<const bf16_t*>(v), static_cast<const bf16_t*>(dout), lse2, work,
-                     static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal, nQB);
+  const bf16_t *Q = static_cast<const bf16_t*>(q), *Kp = static_cast<const bf16_t*>(k),
+               *V = static_cast<const bf16_t*>(v), *DO = static_cast<const bf16_t*>(dout);
+  // EVEN: every tile is full (no per-row bounds checks in the inner loops).
+  if (S % 256 == 0) {
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, dim3(static_cast<unsigned>(B * Hkv * nKB)), dim3(256), 0,
+                       s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
+                       S, Hq, Hkv, c, scale, causal, nKB);
+    rc = KGWE_CHECK_LAUNCH();
+    if (rc) return rc;
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
+                       Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
+                       nQB);
+  } else {
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(static_cast<unsigned>(B * Hkv * nKB)), dim3(256), 0,
+                       s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
+                       S, Hq, Hkv, c, scale, causal, nKB);
+    rc = KGWE_CHECK_LAUNCH();
+    if (rc) return rc;
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
+                       Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
+                       nQB);
+  }
   return KGWE_CHECK_LAUNCH();
 }
 
@@ -660,9 +686,15 @@ KGWE_API int kgwe_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   const long long grid = static_cast<long long>(B) * Hq * nQB;
   if (grid > 0x7fffffff) return -1;
   const float c = scale * 1.4426950408889634f;  // softmax in the exp2 domain
-  hipLaunchKernelGGL(fa_fwd_kernel, dim3(static_cast<unsigned>(grid)), dim3(512), 0, s,
-                     static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
-                     static_cast<const bf16_t*>(v), static_cast<bf16_t*>(o), lse2, S, Hq, Hkv, c,
-                     causal, nQB);
+  if (S % 256 == 0)
+    hipLaunchKernelGGL(fa_fwd_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(512), 0, s,
+                       static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
+                       static_cast<const bf16_t*>(v), static_cast<bf16_t*>(o), lse2, S, Hq, Hkv, c,
+                       causal, nQB);
+  else
+    hipLaunchKernelGGL(fa_fwd_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(512), 0, s,
+                       static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
+                       static_cast<const bf16_t*>(v), static_cast<bf16_t*>(o), lse2, S, Hq, Hkv, c,
+                       causal, nQB);
   return KGWE_CHECK_LAUNCH();
 }

@@ -41,7 +41,7 @@ def test_flash_fwd_matches_reference(B, S, Hq, Hkv, causal, growing_max):
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,causal", [
     (1, 128, 4, 4, True), (2, 256, 8, 2, True), (1, 512, 8, 2, True), (1, 256, 4, 1, False),
-    (1, 200, 4, 2, True)])
+    (1, 200, 4, 2, True), (1, 384, 8, 2, True)])
 def test_flash_bwd_matches_reference(B, S, Hq, Hkv, causal):
     q, k, v = _inputs(B, S, Hq, Hkv, seed=1)
     qh, kh, vh = (t.clone().requires_grad_(True) for t in (q, k, v))
