@@ -48,6 +48,7 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 mfma8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 constexpr int HD = 128;             // head dim
 constexpr int BQ = 128;             // query rows per dQ workgroup
@@ -183,6 +184,15 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
   const int tr_row = 4 * (trG >> 1) + trq;
   const int tr_ch = 2 * (trG & 1) + (trp >> 1);
   const int tr_byte = 8 * (trp & 1);
+  // v_off(C + tr_row, 4 db + tr_ch) + tr_byte for a row base C that is a
+  // multiple of 8: = 256 C + voff[db][(C / 8) & 1] — the swizzle's low bits
+  // depend on C only through (C / 8) & 1, its high bits XOR db with trq.
+  int voff[4][2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi)
+      voff[db][hi] = 256 * tr_row + tr_byte + 64 * (db ^ trq) + 16 * (tr_ch ^ (trG >> 1) ^ (2 * hi));
 
   gload(0);
   swrite(0);
@@ -200,6 +210,8 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
 #pragma unroll
         for (int t = 0; t < 8; ++t)
           sacc[st] = mfma(ld16(&Kc[(st * 32 + lq) * KST + 16 * t + 8 * hh]), qf[t], sacc[st]);
+      // Row max on the RAW scores (c > 0: max commutes with the scaling);
+      // the scale is folded into the exponent's FMA below.
       float mx = -INFINITY;
       const bool edge = (causal && k0 + BKV - 1 > q0) || (!EVEN && k0 + BKV > S);  // wave-uniform
       if (edge) {
@@ -208,21 +220,16 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + st * 32 + acc_row(r, hh);
-            float s = sacc[st][r] * c;
-            if ((!EVEN && key >= S) || (causal && key > qrow)) s = -INFINITY;
-            sacc[st][r] = s;
-            mx = fmaxf(mx, s);
+            if ((!EVEN && key >= S) || (causal && key > qrow)) sacc[st][r] = -INFINITY;
+            mx = fmaxf(mx, sacc[st][r]);
           }
       } else {
 #pragma unroll
         for (int st = 0; st < 2; ++st)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            sacc[st][r] *= c;
-            mx = fmaxf(mx, sacc[st][r]);
-          }
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[st][r]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave)) * c;
       const float m_new = fmaxf(m, mx);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       // Rescale O only when some row's max moved (exact; after the first few
@@ -236,30 +243,36 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
           for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
       }
       m = m_new;
-      float rs = 0.f;
+      // P = 2^(S c - m): one FMA + one v_exp per element; the row sum is
+      // accumulated pairwise (packed adds).
+      f32x2 rs2 = {0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(sacc[st][r] - m_use);
-          sacc[st][r] = p;
-          rs += p;
+        for (int r = 0; r < 16; r += 2) {
+          const float p0 = fast_exp2(fmaf(sacc[st][r], c, -m_use));
+          const float p1 = fast_exp2(fmaf(sacc[st][r + 1], c, -m_use));
+          sacc[st][r] = p0;
+          sacc[st][r + 1] = p1;
+          rs2 += f32x2{p0, p1};
         }
+      const float rs = rs2[0] + rs2[1];
       l += rs + __shfl_xor(rs, 32, kWave);
       // O^T += V^T P : P (key rows, query on lane) is the B operand as is; the
       // V^T fragment (d on the lane, the permuted key order of P on k) comes
-      // from two hardware-transposed reads of the row-major V tile.
+      // from two hardware-transposed reads of the row-major V tile, at the
+      // lane offsets precomputed in voff (+ a compile-time row offset).
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int st = s >> 1, sp = s & 1;
         bf16x8 pb;
 #pragma unroll
         for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[st][8 * sp + j]);
-        const int kbase = st * 32 + 16 * sp + tr_row;
+        const int rowc = 256 * (st * 32 + 16 * sp);
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
-          const u16x4 lo = tr_read(Vc, v_off(kbase, 4 * db + tr_ch) + tr_byte);
-          const u16x4 hi = tr_read(Vc, v_off(kbase + 8, 4 * db + tr_ch) + tr_byte);
+          const u16x4 lo = tr_read(Vc, voff[db][0] + rowc);
+          const u16x4 hi = tr_read(Vc, voff[db][1] + rowc + 256 * 8);
           oacc[db] = mfma(cat44(lo, hi), pb, oacc[db]);
         }
       }
@@ -323,19 +336,37 @@ __device__ __forceinline__ int a_off(int row, int ch) {
   return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
-// Row read of the 16-B chunk `ch` of row `row`.
-__device__ __forceinline__ bf16x8 row_read(const bf16_t* img, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(img) + a_off(row, ch));
+// Lane-dependent parts of the layout-(a) addresses, computed once per kernel:
+//   row read  (row R0 + lk, chunk 2t + hh), R0 % 8 == 0:
+//       a_off = roff[t & 1] + 512 (t >> 1) + 256 R0
+//   transposed read of rows base + tr_row (+8), chunks 4 db + tr_ch,
+//   base % 16 == 0:  a_off + tr_byte = tro[0 or 1] + 256 base + 512 db
+// so every LDS read in the inner loops is a base register + an immediate.
+struct AOffs {
+  int roff[2];
+  int tro[2];
+};
+
+__device__ __forceinline__ AOffs make_aoffs(int lane) {
+  const int lk = lane & 31, hh = lane >> 5;
+  const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
+  const int tr_row = 4 * (trG >> 1) + trq, tr_ch = 2 * (trG & 1) + (trp >> 1), tr_byte = 8 * (trp & 1);
+  AOffs o;
+  o.roff[0] = 2048 * (lk >> 3) + 64 * (lk & 7) + 16 * ((hh) ^ ((lk >> 2) & 3));
+  o.roff[1] = 2048 * (lk >> 3) + 64 * (lk & 7) + 16 * ((2 + hh) ^ ((lk >> 2) & 3));
+  o.tro[0] = 64 * tr_row + 16 * (tr_ch ^ ((tr_row >> 2) & 3)) + tr_byte;
+  o.tro[1] = 2048 + 64 * tr_row + 16 * (tr_ch ^ (((8 + tr_row) >> 2) & 3)) + tr_byte;
+  return o;
 }
 
-// A-operand fragment of a product that sums over the image's ROWS: two
-// hardware-transposed reads of rows base+{0..3} (+8), columns on the lane
-// (same geometry as the forward's V^T reads).
-__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* img, int base, int db, int tr_row, int tr_ch,
-                                          int tr_byte) {
-  const u16x4 lo = tr_read(img, a_off(base + tr_row, 4 * db + tr_ch) + tr_byte);
-  const u16x4 hi = tr_read(img, a_off(base + 8 + tr_row, 4 * db + tr_ch) + tr_byte);
-  return cat44(lo, hi);
+__device__ __forceinline__ bf16x8 row_rd(const bf16_t* img, const AOffs& o, int r0, int t) {
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(img) + o.roff[t & 1] +
+                                          512 * (t >> 1) + 256 * r0);
+}
+
+__device__ __forceinline__ bf16x8 tr_rd(const bf16_t* img, const AOffs& o, int base, int db) {
+  return cat44(tr_read(img, o.tro[0] + 256 * base + 512 * db),
+               tr_read(img, o.tro[1] + 256 * base + 512 * db));
 }
 
 // dK, dV: one workgroup = 128 keys of one (b, kv head); wave = 32 keys.  Q and
@@ -427,8 +458,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
       Dl[buf * BQT + threadIdx.x] = drl;
     }
   };
-  const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
-  const int tr_row = 4 * (trG >> 1) + trq, tr_ch = 2 * (trG & 1) + (trp >> 1), tr_byte = 8 * (trp & 1);
+  const AOffs ao = make_aoffs(lane);
   if (total > 0) {
     gload(0, nqt - 1);
     swrite(0);
@@ -454,8 +484,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
       f32x16 sa = f32x16{}, pa = f32x16{};
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        sa = mfma(row_read(Qc, lk, 2 * t + hh), kf[t], sa);
-        pa = mfma(row_read(Dc, lk, 2 * t + hh), row_read(Vmine, lk, 2 * t + hh), pa);
+        sa = mfma(row_rd(Qc, ao, 0, t), kf[t], sa);
+        pa = mfma(row_rd(Dc, ao, 0, t), row_rd(Vmine, ao, 0, t), pa);
       }
       // P = exp2(S c - lse2), dS = P (dP - delta); row r <-> query qbase + acc_row(r).
       const bool edge = (causal && key0 + 31 > qbase) || (!EVEN && (qbase + BQT > S || key0 + 32 > S));
@@ -487,8 +517,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
         }
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
-          dva[db] = mfma(tr_frag(Dc, 16 * s, db, tr_row, tr_ch, tr_byte), pb, dva[db]);
-          dka[db] = mfma(tr_frag(Qc, 16 * s, db, tr_row, tr_ch, tr_byte), sb, dka[db]);
+          dva[db] = mfma(tr_rd(Dc, ao, 16 * s, db), pb, dva[db]);
+          dka[db] = mfma(tr_rd(Qc, ao, 16 * s, db), sb, dka[db]);
         }
       }
     }
@@ -572,8 +602,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
       *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Vs + buf * VTILE) + off) = vr[i];
     }
   };
-  const int trG = lane >> 4, trq = (lane >> 2) & 3, trp = lane & 3;
-  const int tr_row = 4 * (trG >> 1) + trq, tr_ch = 2 * (trG & 1) + (trp >> 1), tr_byte = 8 * (trp & 1);
+  const AOffs ao = make_aoffs(lane);
   gload(0);
   swrite(0);
   __syncthreads();
@@ -592,8 +621,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         f32x16 sa = f32x16{}, pa = f32x16{};
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          sa = mfma(row_read(Kc, st * 32 + lq, 2 * t + hh), qf[t], sa);
-          pa = mfma(row_read(Vc, st * 32 + lq, 2 * t + hh), df[t], pa);
+          sa = mfma(row_rd(Kc, ao, st * 32, t), qf[t], sa);
+          pa = mfma(row_rd(Vc, ao, st * 32, t), df[t], pa);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -612,7 +641,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           for (int j = 0; j < 8; ++j) sb[j] = f2bf(pa[8 * sp + j]);
 #pragma unroll
           for (int db = 0; db < 4; ++db)
-            dqa[db] = mfma(tr_frag(Kc, st * 32 + 16 * sp, db, tr_row, tr_ch, tr_byte), sb, dqa[db]);
+            dqa[db] = mfma(tr_rd(Kc, ao, st * 32 + 16 * sp, db), sb, dqa[db]);
         }
       }
     }
