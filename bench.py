@@ -53,6 +53,7 @@ def parse(argv=None):
     ap.add_argument("--sched-pods", type=int, default=2000,
                     help="workloads pushed through the extender for the latency p99")
     ap.add_argument("--no-sched", action="store_true")
+    ap.add_argument("--no-busbw", action="store_true", help="skip the RCCL all-reduce busBW probe")
     ap.add_argument("--sdpa", action="store_true", help="force PyTorch SDPA attention")
     ap.add_argument("--parallel", default="zero", choices=["zero", "fsdp"],
                     help="zero: replicated bf16 weights + sharded fp32 optimizer/gradients "
@@ -74,6 +75,30 @@ def run_scheduling_bench(args, world: int) -> dict | None:
         return json.loads(line)
     except Exception as e:  # noqa: BLE001 - report, never fake a number
         print(f"[bench] scheduling benchmark failed: {e}", file=sys.stderr)
+        return None
+
+
+def meter_cost(world: int, tps: float, util: float | None) -> dict | None:
+    """Reference row "cost per training run" (README.md:161): a 1B-token run of
+    this job at the measured throughput and utilisation, metered by the C++
+    cost engine (MI355X on-demand price, utilisation-adjusted)."""
+    try:
+        from kgwe.core import Platform
+
+        p = Platform({})
+        t0, dur = 1.0e9, 1e9 / tps  # seconds for 1B tokens
+        p.cost_start({"uid": "bench-run", "namespace": "bench", "team": "bench",
+                      "gpu_count": world, "tier": "on_demand"}, t0)
+        u = util if util is not None else 0.0
+        for i in range(1, 11):
+            p.cost_sample("bench-run", u, u, t0 + dur * i / 10)
+        rec = p.cost_finalize("bench-run", t0 + dur)
+        return {"run_tokens": int(1e9), "run_hours": round(dur / 3600, 3), "gpus": world,
+                "raw_cost_usd": round(rec["raw_cost"], 2),
+                "adjusted_cost_usd": round(rec["adjusted_cost"], 2),
+                "usd_per_gpu_hour": round(rec["raw_cost"] / (world * dur / 3600), 3)}
+    except Exception as e:  # noqa: BLE001 - optional row, never fake it
+        print(f"[bench] cost metering failed: {e}", file=sys.stderr)
         return None
 
 
@@ -99,6 +124,14 @@ def main(argv=None) -> int:
     if args.gpus != world and info.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
+    # Reference row "142 -> 228 GB/s" (all-reduce bus bandwidth, docs/PRD.md:117-124):
+    # RCCL over xGMI on this job's own ranks, before training allocates memory.
+    busbw = None
+    if world > 1 and not args.no_busbw:
+        from kgwe.parallel import busbw as kbus
+
+        busbw = kbus.torch_sweep(sizes=[1 << 26, 1 << 28, 1 << 30], iters=10, info=info)
+
     tc = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
                      activation_checkpointing=args.ckpt, parallel=args.parallel)
     tr = Trainer(tc, info)
@@ -116,6 +149,7 @@ def main(argv=None) -> int:
 
     if info.is_main:
         p99 = sched["p99_ms"] if sched else None
+        cost = meter_cost(world, tps, util)
         out = {
             "metric": METRIC,
             "value": round(util, 2) if util is not None else None,
@@ -146,6 +180,9 @@ def main(argv=None) -> int:
             "attention": "sdpa" if (args.sdpa or not attn_ops.hip_flash_available())
             else "kgwe_flash_attn",
             "gemm_solutions": "tuned (kgwe/tuning)" if tr.tuned_gemms else "library default",
+            "allreduce_busbw_gbps": (round(busbw["peak_busbw_gbps"], 1) if busbw else None),
+            "allreduce_sweep": busbw["rows"] if busbw else None,
+            "cost": cost,
         }
         print(json.dumps(out), flush=True)
     kdist.barrier(info)

@@ -78,7 +78,8 @@ def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev):
 
 
 def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 50.0,
-        lifetime_s: tuple = (0.5, 3.0), seed: int = 7, timeout_s: float = 300.0) -> dict:
+        lifetime_s: tuple = (0.5, 3.0), seed: int = 7, timeout_s: float = 300.0,
+        tick_s: float = 0.5, reclaim_idle_s: float = 2.0) -> dict:
     from ..controller.kube import KubeClient
     from ..core import LatencyHistogram, Platform, make_fixture
     from ..extender.server import ExtenderServer
@@ -90,7 +91,10 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
     api_p.start()
     api_url = parent.recv()
     kube = KubeClient(api_url)
-    plat = Platform({"enforceBudgets": True})
+    # Housekeeping as the controller runs it (tick: gang expiry, cost sampling,
+    # idle-partition reclaim).  Pod lifetimes here are seconds, not hours, so
+    # the reclaim hysteresis is scaled down with them (production default 60 s).
+    plat = Platform({"enforceBudgets": True, "partitionReclaimIdleSeconds": reclaim_idle_s})
     for i in range(n_nodes):
         name = f"mi355x-{i:03d}"
         plat.add_fake_node(make_fixture(name, 8, 2))
@@ -144,9 +148,25 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
                 plat.release(uid)
             time.sleep(0.01)
 
+    slice_util: list[float] = []
+
+    def partition_sampler():  # time-average of CPX/QPX/DPX slice occupancy
+        while not all_done.is_set():
+            m = plat.partition_metrics()
+            if any(k != "SPX" and v.get("gpus", 0) for k, v in m.get("modes", {}).items()):
+                slice_util.append(m.get("slice_utilization", 0.0))
+            time.sleep(0.1)
+
+    def housekeeping():
+        while not all_done.is_set():
+            plat.tick()
+            time.sleep(tick_s)
+
     expiry: list = []
     threading.Thread(target=consumer, daemon=True).start()
     threading.Thread(target=reaper, daemon=True).start()
+    threading.Thread(target=partition_sampler, daemon=True).start()
+    threading.Thread(target=housekeeping, daemon=True).start()
     time.sleep(0.3)  # scheduler process: first watch established
     t_start = time.perf_counter()
     with lock:
@@ -182,6 +202,11 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
         "throughput_pods_per_s": round(n_bound[0] / wall, 1),
         "core_schedule_p99_ms": round(sm.get("p99_ms", 0.0), 3),
         "partition_reconfigs": pm.get("ops_total", 0),
+        # reference "MIG instance utilization 92 %" (README.md:160): share of
+        # partition slices in use on partitioned GPUs, time-averaged over the run
+        "partition_slice_utilization_pct": (round(100.0 * sum(slice_util) / len(slice_util), 2)
+                                            if slice_util else None),
+        "partition_slice_samples": len(slice_util),
         "topology_optimal_placements": sm.get("topology_optimal", 0),
         "extender_phases_ms": ext.tracer.summary(),
         "processes": "apiserver | kube-scheduler sim | extender+core",

@@ -33,6 +33,7 @@ DEFAULTS = {
     "cost": {"journalPath": "", "enableSpotOptimization": True, "enableRightsizing": True},
     "partitionDryRun": False,
     "autoProvisionPartitions": True,
+    "partitionReclaimIdleSeconds": 60.0,
     "enforceBudgets": True,
     "optimizer": {"target": ""},
     "fakeNodes": 0,
@@ -45,7 +46,8 @@ DEFAULTS = {
 
 def build(cfg: dict):
     plat = Platform({k: cfg[k] for k in ("scheduler", "cost", "partitionDryRun",
-                                         "autoProvisionPartitions", "enforceBudgets")})
+                                         "autoProvisionPartitions", "partitionReclaimIdleSeconds",
+                                         "enforceBudgets")})
     for i in range(int(cfg.get("fakeNodes", 0))):
         plat.add_fake_node(make_fixture(f"mi355x-sim-{i:03d}", 8, 2))
     kube = None

@@ -90,6 +90,9 @@ class Platform:
     # fault injection (fake nodes) --------------------------------------------
     def fake_set_link_up(self, node, a, b, up): self._p.fake_set_link_up(node, a, b, up)
     def fake_set_health(self, node, gpu, status, reason=""): self._p.fake_set_health(node, gpu, status, reason)
+    def fake_set_health_signals(self, node, gpu, signals: dict):
+        self._p.fake_set_health_signals(node, gpu, json.dumps(signals))
+
     def fake_set_util(self, node, gpu, gfx, mem_gb=0.0): self._p.fake_set_util(node, gpu, gfx, mem_gb)
     def fake_set_measured_link(self, node, a, b, gbps): self._p.fake_set_measured_link(node, a, b, gbps)
     def fake_partition_switches(self, node): return self._p.fake_partition_switches(node)

@@ -38,32 +38,40 @@ def native_sweep(ndev: int = 0, sizes=SIZES, iters: int = 20) -> dict:
                      for i in range(n)]}
 
 
-def torch_sweep(sizes=SIZES, iters: int = 20) -> dict:
+def torch_sweep(sizes=SIZES, iters: int = 20, info=None) -> dict:
+    """All-reduce sweep over the default process group.  With ``info`` given
+    the caller owns the group (it is neither created nor destroyed here)."""
     import torch  # noqa: PLC0415
     import torch.distributed as dist  # noqa: PLC0415
 
     from . import dist as kdist  # noqa: PLC0415
 
-    info = kdist.init(force_group=True)
+    own = info is None
+    if own:
+        info = kdist.init(force_group=True)
     n = info.world_size
     rows = []
+    sync = torch.cuda.synchronize if info.device.type == "cuda" else (lambda: None)
     buf = torch.zeros(max(sizes) // 2, dtype=torch.bfloat16, device=info.device)
     for s in sizes:
         x = buf[: s // 2]
         for _ in range(3):
             dist.all_reduce(x)
-        torch.cuda.synchronize()
+        sync()
         kdist.barrier(info)
         t0 = time.perf_counter()
         for _ in range(iters):
             dist.all_reduce(x)
-        torch.cuda.synchronize()
+        sync()
         t = kdist.all_reduce_max((time.perf_counter() - t0) / iters, info)
         alg = s / t / 1e9
         rows.append({"bytes": s, "us": t * 1e6, "algbw_gbps": alg,
                      "busbw_gbps": alg * 2 * (n - 1) / n if n > 1 else 0.0})
-    out = {"driver": "torch", "ndev": n, "rows": rows}
-    kdist.shutdown()
+    del buf
+    out = {"driver": "torch", "ndev": n, "rows": rows,
+           "peak_busbw_gbps": max(r["busbw_gbps"] for r in rows)}
+    if own:
+        kdist.shutdown()
     return out
 
 

@@ -36,6 +36,7 @@ PlatformConfig config_from_json(const std::string& s) {
   c.cost.enable_rightsizing = cc.get("enableRightsizing").as_bool(true);
   c.partition_dry_run = j.get("partitionDryRun").as_bool(false);
   c.auto_provision_partitions = j.get("autoProvisionPartitions").as_bool(true);
+  c.partition_reclaim_idle_s = j.get("partitionReclaimIdleSeconds").as_number(c.partition_reclaim_idle_s);
   c.enforce_budgets = j.get("enforceBudgets").as_bool(true);
   c.master_port = static_cast<int>(j.get("masterPort").as_int(29500));
   c.gpu_resource = j.get("gpuResource").str("amd.com/gpu");
@@ -208,6 +209,11 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("fake_set_health", [](PyPlatform& s, const std::string& node, const std::string& gpu,
                                  const std::string& status, const std::string& reason) {
         s.fake(node).set_health(gpu, health_from(status), reason);
+        s.p->discovery()->refresh_node(node);
+      })
+      .def("fake_set_health_signals", [](PyPlatform& s, const std::string& node, const std::string& gpu,
+                                         const std::string& js) {
+        s.fake(node).set_health_signals(gpu, Json::parse(js));
         s.p->discovery()->refresh_node(node);
       })
       .def("fake_set_util", [](PyPlatform& s, const std::string& node, const std::string& gpu,

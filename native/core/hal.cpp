@@ -5,6 +5,8 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <memory>
+#include <vector>
 #include <sstream>
 
 #include <amd_smi/amdsmi.h>
@@ -151,8 +153,31 @@ void FakeHal::set_health(const std::string& gpu, HealthStatus s, const std::stri
   GpuDevice* g = node_.gpu(gpu);
   if (!g) return;
   g->health.status = s;
+  g->health.pinned = true;
   g->health.reasons.clear();
   if (!reason.empty()) g->health.reasons.push_back(reason);
+}
+
+void FakeHal::set_health_signals(const std::string& gpu, const Json& j) {
+  std::lock_guard<std::mutex> lk(mu_);
+  GpuDevice* g = node_.gpu(gpu);
+  if (!g) return;
+  Health& h = g->health;
+  h.ecc_correctable = j.get("ecc_correctable").as_int(h.ecc_correctable);
+  h.ecc_uncorrectable = j.get("ecc_uncorrectable").as_int(h.ecc_uncorrectable);
+  h.ecc_deferred = j.get("ecc_deferred").as_int(h.ecc_deferred);
+  h.xgmi_errors = static_cast<int>(j.get("xgmi_errors").as_int(h.xgmi_errors));
+  h.xgmi_links_down = static_cast<int>(j.get("xgmi_links_down").as_int(h.xgmi_links_down));
+  h.retired_pages = j.get("retired_pages").as_int(h.retired_pages);
+  h.pending_retired_pages = j.get("pending_retired_pages").as_int(h.pending_retired_pages);
+  if (j.get("throttle").is_array()) {
+    h.throttle_reasons.clear();
+    for (const auto& t : j.get("throttle").items()) h.throttle_reasons.push_back(t.str());
+  }
+  h.pinned = false;
+  int down = 0;
+  for (const auto& l : g->links) down += !l.up;
+  apply_health_policy(h, down);
 }
 
 void FakeHal::set_util(const std::string& gpu, double gfx, double mem_used_gb) {
@@ -201,6 +226,11 @@ struct AmdSmiHal::Impl {
   KGWE_SMI_FN(amdsmi_set_gpu_memory_partition)
   KGWE_SMI_FN(amdsmi_get_temp_metric)
   KGWE_SMI_FN(amdsmi_get_power_info)
+  // optional (older libamd_smi builds may lack them): resolved without failing
+  KGWE_SMI_FN(amdsmi_gpu_xgmi_error_status)
+  KGWE_SMI_FN(amdsmi_get_gpu_xgmi_link_status)
+  KGWE_SMI_FN(amdsmi_get_gpu_bad_page_info)
+  KGWE_SMI_FN(amdsmi_get_violation_status)
 #undef KGWE_SMI_FN
   std::vector<amdsmi_processor_handle> handles;
   std::vector<std::string> uuids;
@@ -241,6 +271,13 @@ AmdSmiHal::AmdSmiHal() : impl_(new Impl) {
   KGWE_SMI_SYM(amdsmi_get_temp_metric)
   KGWE_SMI_SYM(amdsmi_get_power_info)
 #undef KGWE_SMI_SYM
+#define KGWE_SMI_OPT(name) \
+  impl_->name = reinterpret_cast<decltype(impl_->name)>(dlsym(impl_->so, #name));
+  KGWE_SMI_OPT(amdsmi_gpu_xgmi_error_status)
+  KGWE_SMI_OPT(amdsmi_get_gpu_xgmi_link_status)
+  KGWE_SMI_OPT(amdsmi_get_gpu_bad_page_info)
+  KGWE_SMI_OPT(amdsmi_get_violation_status)
+#undef KGWE_SMI_OPT
   if (impl_->amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) {
     err_ = "amdsmi_init failed (no amdgpu driver?)";
     return;
@@ -379,15 +416,55 @@ void AmdSmiHal::refresh_telemetry(NodeTopology& n) {
     if (I.amdsmi_get_power_info(h, &pw) == AMDSMI_STATUS_SUCCESS)
       g.util.power_w = static_cast<double>(pw.current_socket_power ? pw.current_socket_power
                                                                    : pw.average_socket_power);
-    // Health policy: uncorrectable ECC => Unhealthy; deferred => Degraded.
-    g.health.reasons.clear();
-    g.health.status = HealthStatus::Healthy;
-    if (g.health.ecc_uncorrectable > 0) {
-      g.health.status = HealthStatus::Unhealthy;
-      g.health.reasons.push_back("uncorrectable ECC errors");
-    } else if (g.health.ecc_deferred > 0) {
-      g.health.status = HealthStatus::Degraded;
-      g.health.reasons.push_back("deferred ECC errors");
+    if (I.amdsmi_gpu_xgmi_error_status) {
+      amdsmi_xgmi_status_t xs;
+      if (I.amdsmi_gpu_xgmi_error_status(h, &xs) == AMDSMI_STATUS_SUCCESS)
+        g.health.xgmi_errors = xs == AMDSMI_XGMI_STATUS_NO_ERRORS ? 0
+                               : xs == AMDSMI_XGMI_STATUS_ERROR   ? 1
+                                                                  : 2;
+    }
+    if (I.amdsmi_get_gpu_xgmi_link_status) {
+      amdsmi_xgmi_link_status_t ls;
+      std::memset(&ls, 0, sizeof ls);
+      if (I.amdsmi_get_gpu_xgmi_link_status(h, &ls) == AMDSMI_STATUS_SUCCESS) {
+        int down = 0;
+        for (uint32_t k = 0; k < ls.total_links && k < AMDSMI_MAX_NUM_XGMI_LINKS; ++k)
+          down += ls.status[k] == AMDSMI_XGMI_LINK_DOWN;
+        g.health.xgmi_links_down = down;
+      }
+    }
+    if (I.amdsmi_get_gpu_bad_page_info) {
+      uint32_t np = 0;
+      if (I.amdsmi_get_gpu_bad_page_info(h, &np, nullptr) == AMDSMI_STATUS_SUCCESS) {
+        std::vector<amdsmi_retired_page_record_t> rec(np);
+        int64_t retired = 0, pending = 0;
+        if (np && I.amdsmi_get_gpu_bad_page_info(h, &np, rec.data()) == AMDSMI_STATUS_SUCCESS)
+          for (uint32_t k = 0; k < np; ++k) {
+            retired += rec[k].status == AMDSMI_MEM_PAGE_STATUS_RESERVED;
+            pending += rec[k].status == AMDSMI_MEM_PAGE_STATUS_PENDING;
+          }
+        g.health.retired_pages = retired;
+        g.health.pending_retired_pages = pending;
+      }
+    }
+    if (I.amdsmi_get_violation_status) {
+      // ~100 KB (per-XCP x XCC arrays): heap, not the agent thread's stack.
+      auto vs = std::make_unique<amdsmi_violation_status_t>();
+      std::memset(vs.get(), 0, sizeof *vs);
+      g.health.throttle_reasons.clear();
+      if (I.amdsmi_get_violation_status(h, vs.get()) == AMDSMI_STATUS_SUCCESS) {
+        auto on = [](uint8_t v) { return v == 1; };  // 0xff = unsupported
+        if (on(vs->active_prochot_thrm)) g.health.throttle_reasons.push_back("prochot");
+        if (on(vs->active_ppt_pwr)) g.health.throttle_reasons.push_back("ppt_power");
+        if (on(vs->active_socket_thrm)) g.health.throttle_reasons.push_back("socket_thermal");
+        if (on(vs->active_vr_thrm)) g.health.throttle_reasons.push_back("vr_thermal");
+        if (on(vs->active_hbm_thrm)) g.health.throttle_reasons.push_back("hbm_thermal");
+      }
+    }
+    if (!g.health.pinned) {
+      int down = 0;
+      for (const auto& l : g.links) down += !l.up;
+      apply_health_policy(g.health, down);
     }
   }
   n.updated_ns = now_ns();

@@ -45,7 +45,11 @@ class FakeHal : public Hal {
 
   // Fault / state injection (tests, chaos drills).
   void set_link_up(const std::string& a, const std::string& b, bool up);
-  void set_health(const std::string& gpu, HealthStatus s, const std::string& reason);
+  void set_health(const std::string& gpu, HealthStatus s, const std::string& reason);  // pinned
+  // Raw RAS / xGMI / throttle signals (keys of the fixture "health" object);
+  // status is re-derived by apply_health_policy.  Chaos drills: ECC storms,
+  // page retirement, xGMI error bursts.
+  void set_health_signals(const std::string& gpu, const Json& signals);
   void set_util(const std::string& gpu, double gfx_activity, double mem_used_gb);
   void set_measured_link(const std::string& a, const std::string& b, double gbps);
   Json fixture() const;

@@ -177,6 +177,12 @@ void MetricRegistry::declare_kgwe_families() {
   declare("kgwe_gpu_health_status", M::Gauge, "1 healthy, 0.5 degraded, 0 unhealthy", {"gpu_uuid", "node"});
   declare("kgwe_gpu_hbm_bandwidth_gbps", M::Gauge, "Measured HBM copy bandwidth (HIP probe)", {"gpu_uuid", "node"});
   declare("kgwe_gpu_ecc_errors_total", M::Gauge, "ECC error counts", {"gpu_uuid", "node", "type"});
+  declare("kgwe_gpu_retired_pages", M::Gauge, "HBM pages retired / pending retirement",
+          {"gpu_uuid", "node", "state"});
+  declare("kgwe_gpu_xgmi_errors", M::Gauge, "xGMI error state (0 none, 1 error, 2 multiple)",
+          {"gpu_uuid", "node"});
+  declare("kgwe_gpu_throttle_active", M::Gauge, "Active throttle / violation reasons",
+          {"gpu_uuid", "node", "reason"});
   // Partitions (MIG analogue)
   declare("kgwe_gpu_partition_mode", M::Gauge, "1 for the active compute/memory partition mode",
           {"gpu_uuid", "node", "compute", "memory"});

@@ -166,8 +166,45 @@ GpuDevice gpu_from_json(const Json& j, const std::string& node) {
   g.health.ecc_uncorrectable = h.get("ecc_uncorrectable").as_int(0);
   g.health.ecc_deferred = h.get("ecc_deferred").as_int(0);
   g.health.xgmi_errors = static_cast<int>(h.get("xgmi_errors").as_int(0));
+  g.health.xgmi_links_down = static_cast<int>(h.get("xgmi_links_down").as_int(0));
+  g.health.retired_pages = h.get("retired_pages").as_int(0);
+  g.health.pending_retired_pages = h.get("pending_retired_pages").as_int(0);
   for (const auto& r : h.get("throttle").items()) g.health.throttle_reasons.push_back(r.str());
+  g.health.pinned = h.get("pinned").as_bool(h.get("status").is_string());
+  if (!g.health.pinned) {
+    int down = 0;
+    for (const auto& l : g.links) down += !l.up;
+    apply_health_policy(g.health, down);
+  }
   return g;
+}
+
+void apply_health_policy(Health& h, int links_down_in_topology) {
+  h.status = HealthStatus::Healthy;
+  h.reasons.clear();
+  auto degrade = [&](const std::string& why) {
+    if (h.status == HealthStatus::Healthy) h.status = HealthStatus::Degraded;
+    h.reasons.push_back(why);
+  };
+  auto note = [&](const std::string& why) { h.reasons.push_back(why); };
+  auto fail = [&](const std::string& why) {
+    h.status = HealthStatus::Unhealthy;
+    h.reasons.push_back(why);
+  };
+  if (h.ecc_uncorrectable > 0) fail(std::to_string(h.ecc_uncorrectable) + " uncorrectable ECC errors");
+  if (h.retired_pages >= kRetiredPageLimit)
+    fail(std::to_string(h.retired_pages) + " retired HBM pages (limit " + std::to_string(kRetiredPageLimit) + ")");
+  if (h.ecc_deferred > 0) degrade(std::to_string(h.ecc_deferred) + " deferred ECC errors");
+  if (h.ecc_correctable >= kCorrectableStorm)
+    degrade("correctable ECC storm (" + std::to_string(h.ecc_correctable) + ")");
+  if (h.pending_retired_pages > 0)
+    degrade(std::to_string(h.pending_retired_pages) + " HBM pages pending retirement");
+  if (h.xgmi_errors > 0) degrade("xGMI errors reported");
+  const int down = h.xgmi_links_down > links_down_in_topology ? h.xgmi_links_down : links_down_in_topology;
+  // A down link is excluded per link by the group search; the GPU itself
+  // stays schedulable (single-GPU and partition work never crosses it).
+  if (down > 0) note(std::to_string(down) + " xGMI link(s) down");
+  for (const auto& t : h.throttle_reasons) note("throttling: " + t);
 }
 
 Json to_json(const GpuDevice& g) {
@@ -239,6 +276,10 @@ Json to_json(const GpuDevice& g) {
   h["ecc_uncorrectable"] = g.health.ecc_uncorrectable;
   h["ecc_deferred"] = g.health.ecc_deferred;
   h["xgmi_errors"] = g.health.xgmi_errors;
+  h["xgmi_links_down"] = g.health.xgmi_links_down;
+  h["retired_pages"] = g.health.retired_pages;
+  h["pending_retired_pages"] = g.health.pending_retired_pages;
+  h["pinned"] = g.health.pinned;
   Json th = Json::array();
   for (const auto& r : g.health.throttle_reasons) th.push_back(r);
   h["throttle"] = th;

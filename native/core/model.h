@@ -73,8 +73,25 @@ struct Health {
   int64_t ecc_uncorrectable = 0;
   int64_t ecc_deferred = 0;
   int xgmi_errors = 0;
-  std::vector<std::string> throttle_reasons;
+  int xgmi_links_down = 0;          // amdsmi_get_gpu_xgmi_link_status: links reported DOWN
+  int64_t retired_pages = 0;        // HBM pages retired (amdsmi_get_gpu_bad_page_info)
+  int64_t pending_retired_pages = 0;  // marked bad, retired at the next reset
+  std::vector<std::string> throttle_reasons;  // active violations: prochot, socket/vr/hbm thermal, ppt
+  bool pinned = false;              // status set by an operator / fault injection: policy leaves it
 };
+
+// Health policy shared by every HAL backend (reference GPUHealth,
+// src/discovery/types.go:269-321; it only consumed `Healthy`).  Derives
+// status + reasons from the raw RAS / xGMI / throttle signals:
+//   Unhealthy: uncorrectable ECC, or retired pages >= kRetiredPageLimit
+//   Degraded : deferred ECC, correctable-ECC storm, pages pending retirement,
+//              xGMI errors
+//   reason only: xGMI links down (the group search drops the link, not the
+//              GPU) and active throttling (prochot, PPT power, socket / VR /
+//              HBM thermal — a GPU at full load routinely sits at its cap).
+constexpr int64_t kRetiredPageLimit = 64;
+constexpr int64_t kCorrectableStorm = 1000;
+void apply_health_policy(Health& h, int links_down_in_topology = 0);
 
 // One schedulable slice of a partitioned GPU (CPX: 8 per GPU, one per XCD).
 struct PartitionInstance {

@@ -313,6 +313,33 @@ std::vector<PartitionOp> PartitionController::reclaim_idle(bool plan_only) {
   return out;
 }
 
+std::vector<PartitionOp> PartitionController::reclaim_idle_after(double now_s, double min_idle_s) {
+  std::vector<PartitionOp> out;
+  auto snap = disc_->snapshot();
+  std::vector<std::pair<std::string, const GpuDevice*>> due;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::map<std::string, double> seen;
+    for (const auto& kv : snap->nodes)
+      for (const auto& g : kv.second.gpus) {
+        if (g.partition.compute == ComputePartition::SPX || !gpu_idle(g)) continue;
+        auto it = idle_since_.find(g.uuid);
+        const double t0 = it == idle_since_.end() ? now_s : it->second;
+        seen[g.uuid] = t0;
+        if (now_s - t0 >= min_idle_s) due.emplace_back(kv.first, &g);
+      }
+    idle_since_.swap(seen);  // busy / SPX GPUs drop out of the idle map
+  }
+  for (const auto& d : due) {
+    out.push_back(execute(d.first, *d.second, ComputePartition::SPX,
+                          "reclaim partitioned GPU idle for >= " + std::to_string(min_idle_s) + " s",
+                          false));
+    std::lock_guard<std::mutex> lk(mu_);
+    idle_since_.erase(d.second->uuid);
+  }
+  return out;
+}
+
 std::vector<PartitionOp> PartitionController::operations() const {
   std::lock_guard<std::mutex> lk(mu_);
   return ops_;

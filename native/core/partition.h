@@ -87,6 +87,11 @@ class PartitionController {
   std::vector<PartitionOp> rebalance(const std::string& strategy, bool plan_only = false);
   // Return idle partitioned GPUs with no slice in use back to SPX.
   std::vector<PartitionOp> reclaim_idle(bool plan_only = false);
+  // Hysteresis variant driven by the housekeeping tick (reference: the MIG
+  // controller's auto-rebalance, src/sharing/mig_controller.go:39-69): a
+  // partitioned GPU returns to SPX only after it has stayed idle for
+  // `min_idle_s`, so a burst of partition pods does not thrash modes.
+  std::vector<PartitionOp> reclaim_idle_after(double now_s, double min_idle_s);
 
   std::vector<PartitionOp> operations() const;
   PartitionMetrics metrics() const;
@@ -103,6 +108,7 @@ class PartitionController {
   bool dry_run_;
   mutable std::mutex mu_;
   std::map<std::string, PartitionStrategy> strategies_;
+  std::map<std::string, double> idle_since_;  // partitioned GPU uuid -> first idle tick
   std::vector<PartitionOp> ops_;
   int next_op_ = 1;
 };

@@ -423,6 +423,8 @@ void Platform::tick(double now_s) {
       }
     if (n) cost_->sample(a.uid, gfx / n, mem / n, now_s);
   }
+  if (cfg_.partition_reclaim_idle_s >= 0)
+    part_->reclaim_idle_after(now_s, cfg_.partition_reclaim_idle_s);
   refresh_gauges(now_s);
 }
 
@@ -432,6 +434,7 @@ void Platform::refresh_gauges(double now_s) {
                         "kgwe_gpu_umc_activity_percent", "kgwe_gpu_memory_used_bytes",
                         "kgwe_gpu_memory_total_bytes", "kgwe_gpu_temperature_celsius", "kgwe_gpu_power_watts",
                         "kgwe_gpu_health_status", "kgwe_gpu_hbm_bandwidth_gbps", "kgwe_gpu_ecc_errors_total",
+                        "kgwe_gpu_retired_pages", "kgwe_gpu_xgmi_errors", "kgwe_gpu_throttle_active",
                         "kgwe_gpu_partition_mode", "kgwe_partition_instance_count",
                         "kgwe_partition_instance_utilization_percent", "kgwe_xgmi_bandwidth_gbps",
                         "kgwe_xgmi_link_status", "kgwe_pcie_bandwidth_gbps", "kgwe_topology_score",
@@ -460,6 +463,12 @@ void Platform::refresh_gauges(double now_s) {
       if (g.hbm_measured_gbps > 0) reg_->set("kgwe_gpu_hbm_bandwidth_gbps", {g.uuid, n.name}, g.hbm_measured_gbps);
       reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "correctable"}, static_cast<double>(g.health.ecc_correctable));
       reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "uncorrectable"}, static_cast<double>(g.health.ecc_uncorrectable));
+      reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "deferred"}, static_cast<double>(g.health.ecc_deferred));
+      reg_->set("kgwe_gpu_retired_pages", {g.uuid, n.name, "retired"}, static_cast<double>(g.health.retired_pages));
+      reg_->set("kgwe_gpu_retired_pages", {g.uuid, n.name, "pending"},
+                static_cast<double>(g.health.pending_retired_pages));
+      reg_->set("kgwe_gpu_xgmi_errors", {g.uuid, n.name}, static_cast<double>(g.health.xgmi_errors));
+      for (const auto& t : g.health.throttle_reasons) reg_->set("kgwe_gpu_throttle_active", {g.uuid, n.name, t}, 1.0);
       reg_->set("kgwe_gpu_partition_mode", {g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0);
       reg_->set("kgwe_partition_instance_count", {g.uuid, n.name, to_string(g.partition.compute)},
                 static_cast<double>(g.partition.instances.size()));

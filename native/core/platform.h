@@ -33,6 +33,8 @@ struct PlatformConfig {
   CostEngineConfig cost;
   bool partition_dry_run = false;
   bool auto_provision_partitions = true;
+  // Idle partitioned GPUs go back to SPX after this many seconds (<0: never).
+  double partition_reclaim_idle_s = 60.0;
   bool enforce_budgets = true;
   int master_port = 29500;
   std::string gpu_resource = "amd.com/gpu";

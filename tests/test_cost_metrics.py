@@ -115,3 +115,14 @@ def test_prometheus_exposition_has_label_sets(plat):
     assert 'kgwe_active_workloads{namespace="ml",workload_type="Training"} 1' in text
     fams = plat.raw.metric_families()
     assert len(fams) >= 27
+
+
+def test_bench_cost_row_is_metered_by_engine():
+    import bench
+
+    c = bench.meter_cost(8, 160000.0, 99.0)
+    assert c["gpus"] == 8 and c["run_tokens"] == 10**9
+    assert c["run_hours"] == pytest.approx(1e9 / 160000.0 / 3600, rel=1e-3)
+    # high utilisation earns the engine's efficiency discount, never a surcharge
+    assert 0 < c["adjusted_cost_usd"] <= c["raw_cost_usd"]
+    assert c["raw_cost_usd"] == pytest.approx(c["usd_per_gpu_hour"] * 8 * c["run_hours"], rel=1e-2)

@@ -150,3 +150,23 @@ def test_sharded_dp_world2_matches_single_process(tmp_path, bucket_elems, overla
         assert d.mean().item() < 0.02 * LR * STEPS, (i, d.mean().item())
         assert (d > 0.5 * LR).float().mean().item() < 0.01, i
     assert r0["losses"] != r1["losses"]  # ranks really saw different data
+
+
+def _busbw_rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from kgwe.parallel import busbw, dist as kdist
+
+    info = kdist.init(backend="gloo", force_group=True)
+    res = busbw.torch_sweep(sizes=[1 << 16, 1 << 20], iters=2, info=info)
+    assert dist.is_initialized()  # caller-owned group survives the sweep
+    if rank == 0:
+        torch.save({"peak": res["peak_busbw_gbps"], "n": len(res["rows"]), "ndev": res["ndev"]}, out)
+    kdist.shutdown()
+
+
+def test_busbw_sweep_world2_on_caller_group(tmp_path):
+    out = str(tmp_path / "bw.pt")
+    mp.spawn(_busbw_rank, args=(2, _port(), out), nprocs=2, join=True)
+    r = torch.load(out, weights_only=True)
+    assert r["ndev"] == 2 and r["n"] == 2 and r["peak"] > 0

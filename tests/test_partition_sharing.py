@@ -71,6 +71,34 @@ def test_reclaim_idle_partitioned_gpus(plat):
     assert "CPX" not in plat.partition_metrics()["modes"]
 
 
+def test_tick_reclaims_only_after_idle_hysteresis():
+    p = Platform({"partitionReclaimIdleSeconds": 30.0})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    d = p.schedule(part_wl("a"))
+    assert d["ok"] and p.fake_partition_switches("n0") == 1
+    p.tick(100.0)  # slice in use: not idle
+    p.release("a", 101.0)
+    p.tick(102.0)  # idle clock starts
+    p.tick(120.0)
+    assert p.partition_metrics()["modes"]["CPX"]["gpus"] == 1, "reclaimed before the hysteresis"
+    assert p.schedule(part_wl("b"))["ok"]  # reuses the slice, no mode switch
+    assert p.fake_partition_switches("n0") == 1
+    p.tick(140.0)  # busy again: idle clock resets
+    p.release("b", 141.0)
+    p.tick(150.0)
+    p.tick(175.0)
+    assert "CPX" in p.partition_metrics()["modes"]
+    p.tick(181.0)
+    assert "CPX" not in p.partition_metrics()["modes"]
+    assert p.fake_partition_switches("n0") == 2
+    never = Platform({"partitionReclaimIdleSeconds": -1})
+    never.add_fake_node(make_fixture("n0", 8, 2))
+    never.ensure_partitions("CPX", 8)
+    never.tick(0.0)
+    never.tick(1e6)
+    assert never.partition_metrics()["modes"]["CPX"]["gpus"] == 1
+
+
 def test_dry_run_does_not_actuate():
     p = Platform({"partitionDryRun": True})
     p.add_fake_node(make_fixture("d0", 8, 2))

@@ -224,3 +224,48 @@ def test_topology_hints(plat):
     hs = plat.hints(4)
     assert hs and hs[0]["score"] >= 80 and len(hs[0]["gpus"]) == 4
     assert "fully connected xGMI group" in hs[0]["reasons"]
+
+
+@pytest.mark.parametrize("signals,status,reason", [
+    ({"ecc_uncorrectable": 2}, "Unhealthy", "uncorrectable ECC"),
+    ({"retired_pages": 64}, "Unhealthy", "retired HBM pages"),
+    ({"retired_pages": 3}, "Healthy", None),
+    ({"pending_retired_pages": 1}, "Degraded", "pending retirement"),
+    ({"ecc_correctable": 5000}, "Degraded", "ECC storm"),
+    ({"ecc_correctable": 10}, "Healthy", None),
+    ({"ecc_deferred": 1}, "Degraded", "deferred ECC"),
+    ({"xgmi_errors": 1}, "Degraded", "xGMI errors"),
+    ({"xgmi_links_down": 1}, "Healthy", "link(s) down"),
+    ({"throttle": ["hbm_thermal"]}, "Healthy", "throttling: hbm_thermal"),
+])
+def test_health_policy_from_ras_signals(plat, signals, status, reason):
+    """Fault injection through the fake amd-smi: raw RAS /
+    xGMI / throttle signals -> the shared health policy -> schedulability."""
+    gpu = "GPU-n0-02"
+    plat.fake_set_health_signals("n0", gpu, signals)
+    g = next(x for x in plat.node("n0")["gpus"] if x["uuid"] == gpu)
+    assert g["health"]["status"] == status
+    if reason:
+        assert any(reason in r for r in g["health"]["reasons"]), g["health"]["reasons"]
+    d = plat.schedule({"metadata": {"name": "all", "uid": "all"},
+                       "spec": {"gpuRequirements": {"count": 8}}})
+    assert d["ok"]
+    # a whole-node job needs every GPU of the node healthy
+    assert (d["node"] == "n0") == (status == "Healthy"), d["node"]
+
+
+def test_health_signals_round_trip_and_recover(plat):
+    gpu = "GPU-n0-05"
+    plat.fake_set_health_signals("n0", gpu, {"ecc_uncorrectable": 1, "retired_pages": 7})
+    snap = plat.node("n0")
+    h = next(x for x in snap["gpus"] if x["uuid"] == gpu)["health"]
+    assert h["retired_pages"] == 7 and h["status"] == "Unhealthy" and not h["pinned"]
+    # agent push -> controller: the node JSON re-derives the same status
+    from kgwe.core import Platform
+    other = Platform({})
+    other.upsert_node(snap)
+    h2 = next(x for x in other.node("n0")["gpus"] if x["uuid"] == gpu)["health"]
+    assert h2["status"] == "Unhealthy" and h2["retired_pages"] == 7
+    plat.fake_set_health_signals("n0", gpu, {"ecc_uncorrectable": 0})  # after a reset
+    h3 = next(x for x in plat.node("n0")["gpus"] if x["uuid"] == gpu)["health"]
+    assert h3["status"] == "Healthy"
