@@ -7,7 +7,7 @@ TAG     ?= dev
 NPROC   ?= 8
 
 .PHONY: all build rebuild test test-gpu test-all bench bench-sched busbw crds dashboard \
-        helm-lint docker clean sanitize
+        helm-lint docker clean sanitize native-tests
 
 all: build test
 
@@ -46,6 +46,12 @@ helm-lint: crds dashboard
 
 docker:
 	docker build -f docker/Dockerfile -t $(IMAGE):$(TAG) .
+
+native-tests:              ## standalone C++ core tests: plain, TSan, ASan+UBSan builds
+	$(PY) -m kgwe._build --native-tests plain --native-tests tsan --native-tests asan -j $(NPROC)
+	./build/tests/core_tests_plain 2000
+	TSAN_OPTIONS=halt_on_error=1 ./build/tests/core_tests_tsan 400
+	ASAN_OPTIONS=halt_on_error=1 ./build/tests/core_tests_asan 400
 
 sanitize:                  ## host-side ASan/UBSan build of the C++ core + CPU tests
 	KGWE_CORE_SANITIZE=1 $(PY) -m kgwe build --force -j $(NPROC)

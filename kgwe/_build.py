@@ -124,6 +124,40 @@ def build_core(force: bool = False, jobs: int = 8) -> Path | None:
     return _link(objs, LIB / f"_kgwe_core{suffix}", cxx, link, force)
 
 
+SANITIZERS = {
+    "plain": [],
+    "tsan": ["-fsanitize=thread"],
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+}
+
+
+def build_native_tests(flavour: str = "plain", force: bool = False, jobs: int = 8) -> Path:
+    """Standalone C++ test binary over the platform core (no pybind11, no
+    Python): ``build/tests/core_tests_<flavour>``.  ``tsan`` / ``asan`` are
+    the host-side race / memory-error builds."""
+    core_dir = ROOT / "native" / "core"
+    test_dir = ROOT / "native" / "tests"
+    srcs = [s for s in sorted(core_dir.glob("*.cpp")) if s.name != "bindings.cpp"]
+    srcs += sorted(test_dir.glob("*.cpp"))
+    incs = [core_dir, Path("/opt/rocm/include")]
+    cxx = os.environ.get("CXX", "g++")
+    san = SANITIZERS[flavour]
+    flags = ["-O1" if san else "-O2", "-g", "-std=c++17", "-Wall", "-Wextra",
+             "-Wno-unused-parameter", "-fno-omit-frame-pointer", *san]
+    global OBJ
+    saved, OBJ = OBJ, ROOT / "build" / f"obj-tests-{flavour}"
+    try:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(lambda s: _compile(s, cxx, flags, incs, force), srcs))
+    finally:
+        OBJ = saved
+    out = ROOT / "build" / "tests" / f"core_tests_{flavour}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    if force or _stale(out, objs):
+        _run([cxx, *san, *[str(o) for o in objs], "-o", str(out), "-ldl", "-lpthread"])
+    return out
+
+
 def build_all(force: bool = False, jobs: int = 8) -> list[Path]:
     out = []
     with cf.ThreadPoolExecutor(3) as ex:
@@ -140,7 +174,11 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--native-tests", choices=sorted(SANITIZERS), action="append",
+                    help="also build the standalone C++ core test binary (flavour)")
     a = ap.parse_args(argv)
+    for fl in a.native_tests or []:
+        print(build_native_tests(fl, a.force, a.jobs).relative_to(ROOT))
     for p in build_all(a.force, a.jobs):
         print(p.relative_to(ROOT))
     return 0

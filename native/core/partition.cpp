@@ -172,7 +172,8 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
   if (!plan_only) {
     // Drain: the GPU was chosen idle; re-verify right before switching.
     op.state = OpState::Draining;
-    if (!gpu_idle(g)) {
+    const bool fenced = !dry_run_ && sched_;
+    if (!gpu_idle(g) || (fenced && !sched_->fence_gpu(g.uuid))) {
       op.state = OpState::Failed;
       op.error = "gpu no longer idle";
     } else if (dry_run_) {
@@ -188,6 +189,7 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
         op.state = OpState::Failed;
         op.error = err;
       }
+      if (fenced) sched_->unfence_gpu(g.uuid);
     }
     op.finished_ns = now_ns();
   }

@@ -365,7 +365,7 @@ std::vector<const GpuDevice*> Scheduler::free_gpus(const NodeTopology& n,
   for (const auto& g : n.gpus) {
     if (!g.healthy()) continue;
     if (g.partition.compute != ComputePartition::SPX || g.partition.switching) continue;
-    if (gpu_owner_.count(g.uuid)) continue;
+    if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid)) continue;
     if (g.memory_free_gb() + 1e-9 < w.min_memory_gb) continue;
     if (!w.arch.empty() && g.arch != w.arch) continue;
     if (!w.model.empty() && g.model.find(w.model) == std::string::npos) continue;
@@ -381,7 +381,7 @@ std::vector<const PartitionInstance*> Scheduler::free_partitions(
     if (!g.healthy() || g.partition.switching) continue;
     if (g.partition.compute != w.partition_mode) continue;
     if (!w.arch.empty() && g.arch != w.arch) continue;
-    if (gpu_owner_.count(g.uuid)) continue;  // whole GPU taken
+    if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid)) continue;  // whole GPU taken / switching
     for (const auto& pi : g.partition.instances) {
       if (pi.in_use || part_owner_.count(pi.id)) continue;
       if (pi.memory_gb + 1e-9 < w.min_memory_gb) continue;
@@ -800,11 +800,38 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
   return s;
 }
 
+bool Scheduler::gpu_has_slice_owner_locked(const std::string& gpu_uuid) const {
+  if (part_owner_.empty()) return false;
+  for (int i = 0; i < 8; ++i)  // slice ids are "<uuid>/p<i>", at most 8 (CPX)
+    if (part_owner_.count(gpu_uuid + "/p" + std::to_string(i))) return true;
+  return false;
+}
+
+bool Scheduler::fence_gpu(const std::string& gpu_uuid) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  if (gpu_owner_.count(gpu_uuid) || gpu_has_slice_owner_locked(gpu_uuid) || fenced_.count(gpu_uuid))
+    return false;
+  fenced_.insert(gpu_uuid);
+  return true;
+}
+
+void Scheduler::unfence_gpu(const std::string& gpu_uuid) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  fenced_.erase(gpu_uuid);
+}
+
+// Caller holds mu_ exclusively.  The score may come from an older topology
+// snapshot than the ledger: a whole GPU is only reservable when none of its
+// slices is held, a slice only when its GPU is not held whole, and neither
+// while the GPU is fenced for a partition switch.
 bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending) {
   for (const auto& g : s.gpus)
-    if (gpu_owner_.count(g)) return false;
-  for (const auto& p : s.partitions)
+    if (gpu_owner_.count(g) || fenced_.count(g) || gpu_has_slice_owner_locked(g)) return false;
+  for (const auto& p : s.partitions) {
     if (part_owner_.count(p)) return false;
+    const std::string gpu = p.substr(0, p.rfind("/p"));
+    if (gpu_owner_.count(gpu) || fenced_.count(gpu)) return false;
+  }
   if (s.gpus.empty() && s.partitions.empty()) return false;
   Allocation a;
   a.uid = w.uid;

@@ -195,6 +195,13 @@ class Scheduler {
 
   // True when the GPU or any of its partition slices is held in the ledger.
   bool gpu_busy(const GpuDevice& g) const;
+  // Partition-switch fence: atomically (under the ledger lock) check that no
+  // whole-GPU or slice reservation holds `gpu_uuid` and bar new ones until
+  // unfence_gpu.  Closes the window between the controller's idle check and
+  // the mode switch, during which a scheduler thread working from an older
+  // snapshot could otherwise reserve the GPU (or a slice of it).
+  bool fence_gpu(const std::string& gpu_uuid);
+  void unfence_gpu(const std::string& gpu_uuid);
   std::vector<Allocation> allocations() const;
   bool allocation(const std::string& uid, Allocation* out) const;
   SchedulerMetrics metrics() const;
@@ -234,6 +241,8 @@ class Scheduler {
   std::unordered_map<std::string, Allocation> allocs_;
   std::unordered_map<std::string, std::string> gpu_owner_;   // gpu uuid -> uid
   std::unordered_map<std::string, std::string> part_owner_;  // partition id -> uid
+  std::set<std::string> fenced_;                             // GPUs mid partition switch
+  bool gpu_has_slice_owner_locked(const std::string& gpu_uuid) const;
   std::unordered_map<std::string, int> node_gpus_used_;      // node -> allocated GPUs
   struct Gang {
     int size = 0;

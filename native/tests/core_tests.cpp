@@ -1,0 +1,283 @@
+// Native unit + concurrency tests for the C++ platform core (SURVEY.md §4
+// test plan item 1, §5.2 race detection).  Plain asserts, no framework; one
+// binary per build flavour (plain, -fsanitize=thread, -fsanitize=address,
+// undefined), driven by tests/test_native_core.py.
+//
+// The reference's only race tooling is `go test -race` with no tests to run
+// (Makefile:81, .github/workflows/ci.yaml:91) while its ledger re-checks and
+// records under separate lock acquisitions (src/scheduler/scheduler.go:630-640,
+// 695-707).  The stress cases below drive schedule / release / extender
+// filter+bind / topology refresh / telemetry / partition reclaim / metrics
+// exposition from many threads at once and check the ledger invariants
+// (no GPU or slice ever has two owners, everything is released at the end);
+// under TSan any unsynchronised access fails the run.
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <random>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cost.h"
+#include "discovery.h"
+#include "hal.h"
+#include "histogram.h"
+#include "metrics.h"
+#include "partition.h"
+#include "platform.h"
+#include "scheduler.h"
+
+using namespace kgwe;
+
+static int g_failures = 0;
+#define CHECK(cond)                                                                      \
+  do {                                                                                   \
+    if (!(cond)) {                                                                       \
+      std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond);     \
+      ++g_failures;                                                                      \
+    }                                                                                    \
+  } while (0)
+
+static std::shared_ptr<Platform> make_platform(int nodes, PlatformConfig cfg = {}) {
+  auto p = std::make_shared<Platform>(cfg);
+  for (int i = 0; i < nodes; ++i) {
+    std::string name = "n" + std::to_string(i);
+    p->discovery()->add_node(name, std::make_shared<FakeHal>(make_mi355x_node_fixture(name, 8, 2)));
+  }
+  p->discovery()->refresh();
+  return p;
+}
+
+static WorkloadRequest gpus(const std::string& uid, int n, bool xgmi = true) {
+  WorkloadRequest w;
+  w.uid = w.name = uid;
+  w.gpu_count = n;
+  w.topology = xgmi && n > 1 ? TopologyPreference::XgmiOptimal : TopologyPreference::None;
+  return w;
+}
+
+static WorkloadRequest slice(const std::string& uid) {
+  WorkloadRequest w;
+  w.uid = w.name = uid;
+  w.gpu_count = 0;
+  w.partition = true;
+  w.partition_mode = ComputePartition::CPX;
+  w.partition_count = 1;
+  w.type = WorkloadType::Inference;
+  return w;
+}
+
+// Ledger invariant: every GPU / slice has at most one owner, and no GPU is
+// held whole while any of its slices is held.
+static bool ledger_consistent(Scheduler& s, size_t* n_gpus = nullptr) {
+  std::set<std::string> seen, whole, sliced;
+  size_t total = 0;
+  for (const auto& a : s.allocations()) {
+    for (const auto& g : a.gpus) {
+      if (!seen.insert(g).second) return false;
+      whole.insert(g);
+      ++total;
+    }
+    for (const auto& p : a.partitions) {
+      if (!seen.insert(p).second) return false;
+      sliced.insert(p.substr(0, p.rfind("/p")));
+      ++total;
+    }
+  }
+  for (const auto& g : sliced)
+    if (whole.count(g)) return false;
+  if (n_gpus) *n_gpus = total;
+  return true;
+}
+
+// Platform path (auto-provisions partitions) for a one-slice CPX request,
+// in GPUWorkload shape.
+static bool platform_schedule(Platform& p, const WorkloadRequest& w) {
+  const std::string body = "{\"metadata\":{\"name\":\"" + w.name + "\",\"uid\":\"" + w.uid +
+                           "\"},\"spec\":{\"workloadType\":\"Inference\",\"gpuRequirements\":"
+                           "{\"count\":0,\"partition\":{\"mode\":\"CPX\",\"count\":1}}}}";
+  return Json::parse(p.schedule(body)).get("ok").as_bool(false);
+}
+
+static void test_topology_fixture() {
+  NodeTopology n = node_from_json(make_mi355x_node_fixture("a", 8, 2));
+  CHECK(n.gpus.size() == 8);
+  CHECK(n.xgmi_fully_connected);
+  for (const auto& g : n.gpus) CHECK(g.links.size() == 7);
+  Json round = to_json(n);
+  NodeTopology m = node_from_json(round);
+  CHECK(m.gpus.size() == 8 && m.gpus[3].uuid == n.gpus[3].uuid);
+}
+
+static void test_schedule_whole_node_and_numa() {
+  auto p = make_platform(1);
+  Scheduler& s = *p->scheduler();
+  Decision d = s.schedule(gpus("two", 2));
+  CHECK(d.ok);
+  Allocation a;
+  CHECK(s.allocation("two", &a) && a.gpus.size() == 2);
+  NodeTopology n;
+  CHECK(p->discovery()->node("n0", &n));
+  CHECK(n.gpu(a.gpus[0])->numa_node == n.gpu(a.gpus[1])->numa_node);  // one NUMA domain
+  CHECK(!s.schedule(gpus("eight", 8)).ok);  // only 6 free
+  CHECK(s.release("two"));
+  CHECK(s.schedule(gpus("eight", 8)).ok);
+  CHECK(s.release("eight"));
+  CHECK(s.allocations().empty());
+}
+
+static void test_health_policy() {
+  Health h;
+  h.ecc_uncorrectable = 1;
+  apply_health_policy(h);
+  CHECK(h.status == HealthStatus::Unhealthy);
+  Health d;
+  d.pending_retired_pages = 2;
+  apply_health_policy(d);
+  CHECK(d.status == HealthStatus::Degraded);
+  Health l;
+  apply_health_policy(l, 1);  // a down link is a reason, not a status change
+  CHECK(l.status == HealthStatus::Healthy && l.reasons.size() == 1);
+}
+
+static void test_histogram_quantile_not_max() {
+  LatencyHistogram hist;
+  for (int i = 0; i < 990; ++i) hist.record_ms(1.0);
+  for (int i = 0; i < 10; ++i) hist.record_ms(500.0);
+  CHECK(hist.quantile_ms(0.99) < 2.0);  // the reference's "P99" would be 500
+  CHECK(hist.max_ms() >= 499.0);
+}
+
+static void test_cost_math() {
+  CostEngine c;
+  UsageRecord r;
+  r.uid = "job";
+  r.ns = "ml";
+  r.gpu_count = 8;
+  CHECK(c.start(r, 0.0).empty());
+  for (int i = 1; i <= 10; ++i) CHECK(c.sample("job", 95.0, 90.0, 360.0 * i));
+  UsageRecord out;
+  CHECK(c.finalize("job", 3600.0, &out));
+  const double price = c.pricing(out.gpu_type).on_demand;
+  CHECK(std::fabs(out.raw_cost - 8 * price) < 0.01);
+  CHECK(out.adjusted_cost <= out.raw_cost);  // >80 % utilisation: efficiency discount
+}
+
+static void test_metrics_exposition_labels() {
+  MetricRegistry reg;
+  reg.declare("kgwe_test_gauge", MetricType::Gauge, "help", {"node", "gpu_uuid"});
+  reg.set("kgwe_test_gauge", {"n\"0", "GPU-1"}, 3.0);
+  std::string text = reg.expose();
+  CHECK(text.find("# TYPE kgwe_test_gauge gauge") != std::string::npos);
+  CHECK(text.find("kgwe_test_gauge{node=\"n\\\"0\",gpu_uuid=\"GPU-1\"} 3") != std::string::npos);
+}
+
+static void test_partition_binpack() {
+  auto p = make_platform(1);
+  std::set<std::string> gpus_used;
+  for (int i = 0; i < 8; ++i) {
+    CHECK(platform_schedule(*p, slice("s" + std::to_string(i))));  // auto-provisions CPX
+    Allocation a;
+    if (p->scheduler()->allocation("s" + std::to_string(i), &a) && a.partitions.size() == 1)
+      gpus_used.insert(a.partitions[0].substr(0, a.partitions[0].rfind("/p")));
+    else
+      CHECK(false);
+  }
+  CHECK(gpus_used.size() == 1);  // one GPU split 8-way
+  CHECK(p->partitions()->metrics().slice_utilization == 1.0);
+}
+
+// Many threads: schedule / release whole-GPU and slice workloads while
+// other threads refresh topology, tick telemetry + reclaim, and scrape.
+static void test_concurrent_ledger_stress(int threads, int iters) {
+  PlatformConfig cfg;
+  cfg.partition_reclaim_idle_s = 0.0;  // reclaim races with slice placement
+  auto p = make_platform(4, cfg);
+  Scheduler& s = *p->scheduler();
+  std::atomic<bool> stop{false};
+  std::atomic<int> violations{0}, scheduled{0};
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      std::mt19937 rng(1234 + t);
+      std::vector<std::string> mine;
+      for (int i = 0; i < iters; ++i) {
+        const std::string uid = "t" + std::to_string(t) + "-" + std::to_string(i);
+        const int kind = static_cast<int>(rng() % 5);
+        WorkloadRequest w = kind == 4 ? slice(uid) : gpus(uid, 1 << (rng() % 3));
+        Decision d;
+        if (kind == 3) {  // extender path: filter -> bind on the first passing node
+          std::vector<std::string> nodes = {"n0", "n1", "n2", "n3"}, passed;
+          s.filter(w, nodes, &passed);
+          if (!passed.empty()) d = s.bind(w, passed[rng() % passed.size()]);
+        } else if (kind == 4) {  // platform path: may convert an idle GPU to CPX
+          d.ok = platform_schedule(*p, w);
+        } else {
+          d = s.schedule(w);
+        }
+        if (d.ok) {
+          mine.push_back(uid);
+          ++scheduled;
+        }
+        if (mine.size() > 3 || (rng() % 3 == 0 && !mine.empty())) {
+          const size_t k = rng() % mine.size();
+          if (!s.release(mine[k])) ++violations;
+          mine.erase(mine.begin() + static_cast<long>(k));
+        }
+        if (!ledger_consistent(s)) ++violations;
+      }
+      for (const auto& u : mine) s.release(u);
+    });
+  std::thread refresher([&] {
+    while (!stop.load()) {
+      p->discovery()->refresh();
+      p->discovery()->refresh_telemetry();
+    }
+  });
+  std::thread ticker([&] {
+    double now = 0;
+    while (!stop.load()) p->tick(now += 1.0);
+  });
+  std::thread scraper([&] {
+    while (!stop.load()) {
+      (void)p->expose_metrics();
+      (void)p->partitions()->metrics();
+      (void)s.metrics();
+      (void)s.drain_events();
+    }
+  });
+  for (auto& th : pool) th.join();
+  stop = true;
+  refresher.join();
+  ticker.join();
+  scraper.join();
+  size_t held = 0;
+  CHECK(violations.load() == 0);
+  CHECK(scheduled.load() > threads * iters / 4);
+  CHECK(ledger_consistent(s, &held));
+  CHECK(held == 0);
+  CHECK(s.allocations().empty());
+  std::printf("  stress: %d threads x %d iters, %d scheduled\n", threads, iters, scheduled.load());
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 400;
+  test_topology_fixture();
+  test_schedule_whole_node_and_numa();
+  test_health_policy();
+  test_histogram_quantile_not_max();
+  test_cost_math();
+  test_metrics_exposition_labels();
+  test_partition_binpack();
+  test_concurrent_ledger_stress(8, iters);
+  if (g_failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", g_failures);
+    return 1;
+  }
+  std::printf("core_tests: all passed\n");
+  return 0;
+}
