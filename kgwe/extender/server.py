@@ -110,15 +110,16 @@ class ExtenderServer:
                             code, data = 500, json.dumps({"error": str(e)}).encode()
                         return self._send(code, data)
                 verb = path[len(outer.prefix):].strip("/")
+                key = outer.trace_key(verb, body) if outer.tracer.exporter else None
                 try:
                     if verb == "filter":
-                        with outer.tracer.phase("filter"):
+                        with outer.tracer.phase("filter", key, verb="filter"):
                             out = outer.platform.filter(body)
                     elif verb == "prioritize":
-                        with outer.tracer.phase("prioritize"):
+                        with outer.tracer.phase("prioritize", key, verb="prioritize"):
                             out = outer.platform.prioritize(body)
                     elif verb == "bind":
-                        with outer.tracer.phase("bind"):
+                        with outer.tracer.phase("bind", key, verb="bind"):
                             out = json.dumps(outer.handle_bind(body))
                     else:
                         return self._send(404, b'{"error":"unknown verb"}')
@@ -153,6 +154,18 @@ class ExtenderServer:
     def url(self) -> str:
         h, p = self.httpd.server_address[:2]
         return f"http://{h}:{p}{self.prefix}"
+
+    @staticmethod
+    def trace_key(verb: str, body: str) -> str | None:
+        """Pod uid of an extender request: one trace per pod scheduling cycle."""
+        try:
+            j = json.loads(body)
+        except ValueError:
+            return None
+        if verb == "bind":
+            return j.get("podUID") or f'{j.get("podNamespace", "")}/{j.get("podName", "")}'
+        meta = (j.get("pod") or j.get("Pod") or {}).get("metadata", {})
+        return meta.get("uid") or f'{meta.get("namespace", "")}/{meta.get("name", "")}'
 
     def handle_bind(self, body: str) -> dict:
         args = json.loads(body)
