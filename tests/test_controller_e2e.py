@@ -237,3 +237,58 @@ def test_leader_election_single_holder_and_failover():
         assert not a.try_acquire_or_renew(t0 + 3.1)
     finally:
         api.stop()
+
+
+def test_mixed_tenancy_training_and_partition_inference(cluster):
+    """BASELINE.json config 5 (examples/mixed-tenancy.yaml): 4-GPU FSDP training
+    + 4 single-slice inference services of another team, optimizer
+    rightsizing and per-team cost attribution."""
+    import yaml
+    from pathlib import Path
+
+    from kgwe.optimizer.optimizer import TelemetryDataPoint, WorkloadOptimizer
+
+    api, kube, plat, ext, rec = cluster
+    docs = [d for d in yaml.safe_load_all((Path(__file__).parents[1] / "examples" /
+                                           "mixed-tenancy.yaml").read_text()) if d]
+    for d in docs:
+        kube.create_cr(d)
+    wait_for(lambda: plat.scheduler_metrics()["allocated_gpus"] == 4
+             and plat.scheduler_metrics()["allocated_partitions"] == 4, timeout=15)
+    allocs = {a["uid"]: a for a in plat.allocations()}
+    train = [a for a in allocs.values() if a["gpus"]]
+    assert len(train) == 1 and len(train[0]["gpus"]) == 4
+    node = plat.node(train[0]["node"])
+    by_uuid = {g["uuid"]: g for g in node["gpus"]}
+    assert len({by_uuid[u]["numa_node"] for u in train[0]["gpus"]}) == 1  # one NUMA domain
+    st = kube.get_cr("GPUWorkload", "research", "llama3-8b-finetune")["status"]
+    assert st["rcclEnv"]["WORLD_SIZE"] == "4" and st["estimatedBandwidth"] > 100
+    # inference: 4 slices bin-packed onto ONE CPX GPU, disjoint from training's GPUs
+    slices = [p for a in allocs.values() for p in a["partitions"]]
+    gpus = {p.rsplit("/p", 1)[0] for p in slices}
+    assert len(slices) == 4 and len(gpus) == 1 and not gpus & set(train[0]["gpus"])
+    # rightsizing: low-utilisation inference telemetry -> CPX recommendation
+    opt = WorkloadOptimizer(learn=False)
+    t0 = time.time()
+    for i in range(30):
+        opt.ingest_telemetry("serve", TelemetryDataPoint(
+            timestamp=t0 + i, gpu_uuid="g0", gpu_utilization=12.0,
+            memory_used_bytes=20 * 2**30, memory_total_bytes=288 * 2**30))
+    pred = opt.predict_resources("serve", {"model_params_billions": 1, "workload_type": "Inference"})
+    assert pred.recommended_partition == "CPX"
+    # completion -> cost records per team; slices metered at 1/8 of a GPU
+    time.sleep(0.3)
+    for name, ns in [("llama3-8b-finetune", "research")] + [(f"llama3-1b-serve-{i}", "serving")
+                                                            for i in range(4)]:
+        kube.patch_pod(ns, f"{name}-gw", {"status": {"phase": "Succeeded"}})
+    wait_for(lambda: not plat.allocations(), timeout=10)
+    cb = {ln["group"]: ln for ln in plat.chargeback("team")["lines"]}
+    assert cb["research"]["workloads"] == 1 and cb["serving"]["workloads"] == 4
+    rates = {}
+    for uid, a in allocs.items():
+        r = plat.cost_record(uid)
+        rates[uid] = r["raw_cost"] / (r["duration_s"] / 3600.0) / r["gpu_count"]
+    train_rate = rates[train[0]["uid"]]
+    for uid, a in allocs.items():
+        if a["partitions"]:
+            assert rates[uid] == pytest.approx(train_rate / 8, rel=0.02)
