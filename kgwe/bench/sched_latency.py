@@ -79,7 +79,7 @@ def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev):
 
 def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 50.0,
         lifetime_s: tuple = (0.5, 3.0), seed: int = 7, timeout_s: float = 300.0,
-        tick_s: float = 0.5, reclaim_idle_s: float = 2.0) -> dict:
+        tick_s: float = 1.0, reclaim_idle_s: float = 2.0) -> dict:
     from ..controller.kube import KubeClient
     from ..core import LatencyHistogram, Platform, make_fixture
     from ..extender.server import ExtenderServer

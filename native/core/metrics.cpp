@@ -123,10 +123,33 @@ static std::string label_str(const std::vector<std::string>& names, const std::v
   return o + "}";
 }
 
+void MetricRegistry::commit(GaugeBatch&& batch) {
+  std::vector<std::pair<std::string, std::map<Labels, Series>>> staged;
+  staged.reserve(batch.fams_.size());
+  for (auto& kv : batch.fams_) {
+    std::map<Labels, Series> series;
+    for (auto& sv : kv.second) series[sv.first].value = sv.second;
+    staged.emplace_back(kv.first, std::move(series));
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& st : staged) {
+      Family* f = find(st.first);
+      for (const auto& s : st.second)
+        if (s.first.size() != f->labels.size()) throw std::runtime_error("label arity mismatch for " + st.first);
+      f->series.swap(st.second);  // old series are freed below, off the lock
+    }
+  }
+}
+
 std::string MetricRegistry::expose() const {
-  std::lock_guard<std::mutex> lk(mu_);
+  std::map<std::string, Family> fams;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    fams = fams_;
+  }
   std::string out;
-  for (const auto& kv : fams_) {
+  for (const auto& kv : fams) {
     const Family& f = kv.second;
     const char* t = f.type == MetricType::Counter ? "counter" : f.type == MetricType::Gauge ? "gauge"
                                                                                             : "histogram";

@@ -18,6 +18,8 @@ namespace kgwe {
 
 enum class MetricType { Counter, Gauge, Histogram };
 
+class GaugeBatch;
+
 class MetricRegistry {
  public:
   using Labels = std::vector<std::string>;  // values, in the family's label order
@@ -32,8 +34,13 @@ class MetricRegistry {
   void clear(const std::string& name);  // drop all series of a family
   double value(const std::string& name, const Labels& lv) const;
   bool has(const std::string& name) const;
+  // Render under a copy: the lock is held only for the copy, so counters
+  // bumped by the scheduling path never wait on text formatting.
   std::string expose() const;
   std::vector<std::string> families() const;
+  // Replace every family named in the batch with exactly the batch's series
+  // (atomically per family: a scrape never sees a half-refreshed family).
+  void commit(GaugeBatch&& batch);
 
   // The kgwe_* families (reference names kept; NVLink -> xGMI, MIG -> partition,
   // plus xGMI link status, partition mode and gfx activity gauges).
@@ -56,6 +63,18 @@ class MetricRegistry {
   Family* find(const std::string& name);
   mutable std::mutex mu_;
   std::map<std::string, Family> fams_;
+};
+
+// Gauge values staged off-lock by a periodic refresh (Platform::tick), then
+// swapped in with MetricRegistry::commit.
+class GaugeBatch {
+ public:
+  void set(const std::string& name, MetricRegistry::Labels lv, double v) { fams_[name][std::move(lv)] = v; }
+  void touch(const std::string& name) { fams_[name]; }  // replace even when it ends up empty
+
+ private:
+  friend class MetricRegistry;
+  std::map<std::string, std::map<MetricRegistry::Labels, double>> fams_;
 };
 
 std::string prom_escape(const std::string& v);

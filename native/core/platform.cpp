@@ -430,6 +430,7 @@ void Platform::tick(double now_s) {
 
 void Platform::refresh_gauges(double now_s) {
   auto snap = disc_->snapshot();
+  GaugeBatch batch;  // built off-lock, swapped in at the end
   for (const char* f : {"kgwe_gpu_count", "kgwe_gpu_utilization_percent", "kgwe_gpu_gfx_activity_percent",
                         "kgwe_gpu_umc_activity_percent", "kgwe_gpu_memory_used_bytes",
                         "kgwe_gpu_memory_total_bytes", "kgwe_gpu_temperature_celsius", "kgwe_gpu_power_watts",
@@ -440,70 +441,71 @@ void Platform::refresh_gauges(double now_s) {
                         "kgwe_xgmi_link_status", "kgwe_pcie_bandwidth_gbps", "kgwe_topology_score",
                         "kgwe_active_workloads", "kgwe_budget_utilization_percent",
                         "kgwe_cost_savings_recommended_dollars", "kgwe_gpu_cost_per_hour_dollars"})
-    reg_->clear(f);
+    batch.touch(f);
   std::set<std::string> owned_parts;
   for (const auto& a : sched_->allocations())
     for (const auto& p : a.partitions) owned_parts.insert(p);
   for (const auto& kv : snap->nodes) {
     const NodeTopology& n = kv.second;
-    reg_->set("kgwe_gpu_count", {n.name}, static_cast<double>(n.gpus.size()));
+    batch.set("kgwe_gpu_count", {n.name}, static_cast<double>(n.gpus.size()));
     std::map<std::string, std::pair<int, int>> slices;  // mode -> (used, total)
     int links_up = 0, links = 0;
     for (const auto& g : n.gpus) {
-      reg_->set("kgwe_gpu_utilization_percent", {g.uuid, n.name, g.model}, g.util.gfx_activity);
-      reg_->set("kgwe_gpu_gfx_activity_percent", {g.uuid, n.name}, g.util.gfx_activity);
-      reg_->set("kgwe_gpu_umc_activity_percent", {g.uuid, n.name}, g.util.umc_activity);
-      reg_->set("kgwe_gpu_memory_used_bytes", {g.uuid, n.name}, g.memory_used_gb * 1073741824.0);
-      reg_->set("kgwe_gpu_memory_total_bytes", {g.uuid, n.name}, g.memory_total_gb * 1073741824.0);
-      reg_->set("kgwe_gpu_temperature_celsius", {g.uuid, n.name}, g.util.temperature_c);
-      reg_->set("kgwe_gpu_power_watts", {g.uuid, n.name}, g.util.power_w);
-      reg_->set("kgwe_gpu_health_status", {g.uuid, n.name},
+      batch.set("kgwe_gpu_utilization_percent", {g.uuid, n.name, g.model}, g.util.gfx_activity);
+      batch.set("kgwe_gpu_gfx_activity_percent", {g.uuid, n.name}, g.util.gfx_activity);
+      batch.set("kgwe_gpu_umc_activity_percent", {g.uuid, n.name}, g.util.umc_activity);
+      batch.set("kgwe_gpu_memory_used_bytes", {g.uuid, n.name}, g.memory_used_gb * 1073741824.0);
+      batch.set("kgwe_gpu_memory_total_bytes", {g.uuid, n.name}, g.memory_total_gb * 1073741824.0);
+      batch.set("kgwe_gpu_temperature_celsius", {g.uuid, n.name}, g.util.temperature_c);
+      batch.set("kgwe_gpu_power_watts", {g.uuid, n.name}, g.util.power_w);
+      batch.set("kgwe_gpu_health_status", {g.uuid, n.name},
                 g.health.status == HealthStatus::Healthy ? 1.0
                 : g.health.status == HealthStatus::Degraded ? 0.5 : 0.0);
-      if (g.hbm_measured_gbps > 0) reg_->set("kgwe_gpu_hbm_bandwidth_gbps", {g.uuid, n.name}, g.hbm_measured_gbps);
-      reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "correctable"}, static_cast<double>(g.health.ecc_correctable));
-      reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "uncorrectable"}, static_cast<double>(g.health.ecc_uncorrectable));
-      reg_->set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "deferred"}, static_cast<double>(g.health.ecc_deferred));
-      reg_->set("kgwe_gpu_retired_pages", {g.uuid, n.name, "retired"}, static_cast<double>(g.health.retired_pages));
-      reg_->set("kgwe_gpu_retired_pages", {g.uuid, n.name, "pending"},
+      if (g.hbm_measured_gbps > 0) batch.set("kgwe_gpu_hbm_bandwidth_gbps", {g.uuid, n.name}, g.hbm_measured_gbps);
+      batch.set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "correctable"}, static_cast<double>(g.health.ecc_correctable));
+      batch.set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "uncorrectable"}, static_cast<double>(g.health.ecc_uncorrectable));
+      batch.set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "deferred"}, static_cast<double>(g.health.ecc_deferred));
+      batch.set("kgwe_gpu_retired_pages", {g.uuid, n.name, "retired"}, static_cast<double>(g.health.retired_pages));
+      batch.set("kgwe_gpu_retired_pages", {g.uuid, n.name, "pending"},
                 static_cast<double>(g.health.pending_retired_pages));
-      reg_->set("kgwe_gpu_xgmi_errors", {g.uuid, n.name}, static_cast<double>(g.health.xgmi_errors));
-      for (const auto& t : g.health.throttle_reasons) reg_->set("kgwe_gpu_throttle_active", {g.uuid, n.name, t}, 1.0);
-      reg_->set("kgwe_gpu_partition_mode", {g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0);
-      reg_->set("kgwe_partition_instance_count", {g.uuid, n.name, to_string(g.partition.compute)},
+      batch.set("kgwe_gpu_xgmi_errors", {g.uuid, n.name}, static_cast<double>(g.health.xgmi_errors));
+      for (const auto& t : g.health.throttle_reasons) batch.set("kgwe_gpu_throttle_active", {g.uuid, n.name, t}, 1.0);
+      batch.set("kgwe_gpu_partition_mode", {g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0);
+      batch.set("kgwe_partition_instance_count", {g.uuid, n.name, to_string(g.partition.compute)},
                 static_cast<double>(g.partition.instances.size()));
       auto& sl = slices[to_string(g.partition.compute)];
       for (const auto& pi : g.partition.instances) {
         sl.second++;
         sl.first += (pi.in_use || owned_parts.count(pi.id)) ? 1 : 0;
       }
-      reg_->set("kgwe_pcie_bandwidth_gbps", {g.uuid, n.name}, g.pcie.bandwidth_gbps);
+      batch.set("kgwe_pcie_bandwidth_gbps", {g.uuid, n.name}, g.pcie.bandwidth_gbps);
       for (const auto& l : g.links) {
-        reg_->set("kgwe_xgmi_bandwidth_gbps", {g.uuid, l.peer_uuid, n.name}, l.up ? l.effective_gbps() : 0.0);
-        reg_->set("kgwe_xgmi_link_status", {g.uuid, l.peer_uuid, n.name}, l.up ? 1.0 : 0.0);
+        batch.set("kgwe_xgmi_bandwidth_gbps", {g.uuid, l.peer_uuid, n.name}, l.up ? l.effective_gbps() : 0.0);
+        batch.set("kgwe_xgmi_link_status", {g.uuid, l.peer_uuid, n.name}, l.up ? 1.0 : 0.0);
         ++links;
         links_up += l.up && l.type == LinkType::XGMI;
       }
     }
     for (const auto& s : slices)
       if (s.first != "SPX")
-        reg_->set("kgwe_partition_instance_utilization_percent", {n.name, s.first},
+        batch.set("kgwe_partition_instance_utilization_percent", {n.name, s.first},
                   s.second.second ? 100.0 * s.second.first / s.second.second : 0.0);
     // Node topology score: 50 base, +30 full xGMI mesh, +20 proportional link health.
     double ts = 50.0 + (n.xgmi_fully_connected ? 30.0 : 0.0) + (links ? 20.0 * links_up / links : 0.0);
-    reg_->set("kgwe_topology_score", {n.name}, ts);
+    batch.set("kgwe_topology_score", {n.name}, ts);
   }
   std::map<std::pair<std::string, std::string>, int> active;
   for (const auto& a : sched_->allocations()) active[{a.ns, to_string(a.type)}]++;
   for (const auto& kv : active)
-    reg_->set("kgwe_active_workloads", {kv.first.first, kv.first.second}, kv.second);
+    batch.set("kgwe_active_workloads", {kv.first.first, kv.first.second}, kv.second);
   for (const auto& b : cost_->budgets(now_s))
-    reg_->set("kgwe_budget_utilization_percent", {b.id, to_string(b.scope)},
+    batch.set("kgwe_budget_utilization_percent", {b.id, to_string(b.scope)},
               b.limit > 0 ? 100.0 * b.spend / b.limit : 0.0);
   std::map<std::string, double> saving;
   for (const auto& r : cost_->recommendations("", "")) saving[r.type] += r.saving;
-  for (const auto& kv : saving) reg_->set("kgwe_cost_savings_recommended_dollars", {kv.first}, kv.second);
-  reg_->set("kgwe_gpu_cost_per_hour_dollars", {"all"}, cost_->running_cost_per_hour());
+  for (const auto& kv : saving) batch.set("kgwe_cost_savings_recommended_dollars", {kv.first}, kv.second);
+  batch.set("kgwe_gpu_cost_per_hour_dollars", {"all"}, cost_->running_cost_per_hour());
+  reg_->commit(std::move(batch));
   reg_->set("kgwe_workload_queue_depth", {}, 0.0);
 }
 

@@ -522,13 +522,16 @@ int Scheduler::topology_score(const NodeTopology& n, const std::vector<const Gpu
         minbw = std::min(minbw, bw);
       }
     }
+    // Domains the group spans (counted before the lookups below, which must
+    // not insert: operator[] on used_numa would add every domain as 0).
+    const int domains = static_cast<int>(used_numa.size());
     // Fragmentation: whole NUMA domains left completely free after placement.
     int whole_free_after = 0;
     for (auto& kv : total_numa) {
-      int left = free_numa[kv.first] - used_numa[kv.first];
+      auto u = used_numa.find(kv.first);
+      const int left = free_numa[kv.first] - (u == used_numa.end() ? 0 : u->second);
       if (left == kv.second) ++whole_free_after;
     }
-    const int domains = static_cast<int>(used_numa.size());
     double obj = (clique ? 1000.0 : 0.0) + 300.0 * std::min(1.0, agg / ideal) +
                  100.0 * (need_domains > 0 ? static_cast<double>(need_domains) / domains : 1.0) +
                  20.0 * whole_free_after + 5.0 * (minbw / cfg_.rated_link_gbps);

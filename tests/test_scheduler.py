@@ -269,3 +269,23 @@ def test_health_signals_round_trip_and_recover(plat):
     plat.fake_set_health_signals("n0", gpu, {"ecc_uncorrectable": 0})  # after a reset
     h3 = next(x for x in plat.node("n0")["gpus"] if x["uuid"] == gpu)["health"]
     assert h3["status"] == "Healthy"
+
+
+def test_group_stays_in_one_numa_domain_after_partial_use():
+    """Regression: the domain count of a candidate group was inflated by
+    map lookups of unused domains, so every 4-GPU group looked like it
+    spanned both sockets and the first combination won (GPUs 1-4 across
+    NUMA 0/1 instead of 4-7 on NUMA 1)."""
+    from kgwe.core import Platform, make_fixture
+
+    p = Platform({})
+    p.add_fake_node(make_fixture("a", 8, 2))
+    assert p.schedule({"metadata": {"name": "one", "uid": "one"},
+                       "spec": {"gpuRequirements": {"count": 1}}})["ok"]
+    d = p.schedule({"metadata": {"name": "t", "uid": "t"},
+                    "spec": {"gpuRequirements": {"count": 4, "topology": {"preference": "xGMIOptimal"}}}})
+    assert d["ok"]
+    numa = {g["uuid"]: g["numa_node"] for g in p.node("a")["gpus"]}
+    alloc = next(a for a in p.allocations() if a["uid"] == "t")
+    assert len({numa[u] for u in alloc["gpus"]}) == 1, alloc["gpus"]
+    assert d["score"] >= 90
