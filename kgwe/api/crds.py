@@ -85,6 +85,12 @@ GPUWORKLOAD_SPEC = _S(
                                                      **{"x-kubernetes-preserve-unknown-fields": True})),
             "affinity": _S(type="object", **{"x-kubernetes-preserve-unknown-fields": True}),
             "maxLatencyMs": _S(type="number", minimum=0)}),
+        "recovery": _S(type="object", description=(
+            "What the controller does when the workload's node is lost or one of its GPUs turns "
+            "Unhealthy (RAS / ECC / xGMI health from amd-smi): Reschedule re-creates the pod "
+            "elsewhere (the job resumes from its own checkpoint), Fail ends the workload."),
+            properties={"policy": _S(type="string", enum=["Reschedule", "Fail"], default="Reschedule"),
+                        "maxRestarts": _S(type="integer", minimum=0, maximum=100, default=3)}),
         "podTemplate": _S(type="object", **{"x-kubernetes-preserve-unknown-fields": True}),
     })
 
@@ -101,6 +107,8 @@ GPUWORKLOAD_STATUS = _S(type="object", properties={
     "conditions": _conditions,
     "startTime": _S(type="string", format="date-time"),
     "completionTime": _S(type="string", format="date-time"),
+    "restarts": _S(type="integer", minimum=0),
+    "lastFailure": _S(type="string"),
     "cost": _S(type="number")})
 
 PARTITIONSTRATEGY_SPEC = _S(type="object", required=["profileDistribution"], properties={

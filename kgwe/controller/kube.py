@@ -108,6 +108,13 @@ class KubeClient:
         return self.request("PATCH", f"/api/v1/nodes/{name}", {"metadata": {"labels": labels}},
                             content_type="application/merge-patch+json")
 
+    def delete_node(self, name: str) -> dict:
+        return self.request("DELETE", f"/api/v1/nodes/{name}", ok=(200, 202, 404))
+
+    def patch_node_status(self, name: str, status: dict) -> dict:
+        return self.request("PATCH", f"/api/v1/nodes/{name}/status", {"status": status},
+                            content_type="application/merge-patch+json")
+
     def list_pods(self, namespace: str | None = None, field_selector: str = "") -> list:
         path = f"/api/v1/namespaces/{namespace}/pods" if namespace else "/api/v1/pods"
         if field_selector:

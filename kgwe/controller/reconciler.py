@@ -13,6 +13,13 @@ which exists in the reference (D1).  Here:
 * Pod termination / deletion -> allocation release + cost finalisation.
 * GPUBudget -> cost-engine budget; status (spend, utilisation, alerts).
 * PartitionStrategy -> registered + rebalanced every rebalanceInterval.
+* Failure detection / recovery (the reference only evicts a
+  deleted node from its cache and leaves its allocations stale): a node that
+  is deleted or stops being Ready, or a GPU of a running allocation that the
+  amd-smi health policy marks Unhealthy, evicts the workloads on it — the
+  allocation is released and, per ``spec.recovery`` (Reschedule, at most
+  maxRestarts times), the GPUWorkload gets a fresh pod that the scheduler
+  places elsewhere; status carries ``restarts`` / ``lastFailure``.
 * Restart safety (checkpoint/resume): on start the ledger is
   rebuilt from the allocation annotations of already-bound pods, so a
   controller restart neither leaks nor double-allocates GPUs.
@@ -37,7 +44,12 @@ def _now_iso() -> str:
     return datetime.now(timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
 
 
-def pod_for_workload(gw: dict) -> dict:
+def pod_name(gw_name: str, restart: int = 0) -> str:
+    """One pod per attempt: a lost node may keep the old pod Terminating."""
+    return f"{gw_name}-gw" if restart == 0 else f"{gw_name}-gw-r{restart}"
+
+
+def pod_for_workload(gw: dict, restart: int = 0) -> dict:
     md = gw["metadata"]
     spec = gw["spec"]
     req = spec["gpuRequirements"]
@@ -70,7 +82,7 @@ def pod_for_workload(gw: dict) -> dict:
                                                  "labels": labels}, "spec": {k: v for k, v in spec.items()
                                                                              if k != "podTemplate"}})
     return {"apiVersion": "v1", "kind": "Pod",
-            "metadata": {"name": f"{md['name']}-gw", "namespace": md.get("namespace", "default"),
+            "metadata": {"name": pod_name(md["name"], restart), "namespace": md.get("namespace", "default"),
                          "labels": labels, "annotations": ann,
                          "ownerReferences": [{"apiVersion": f"{crds.GROUP}/{crds.VERSION}", "kind": "GPUWorkload",
                                               "name": md["name"], "uid": md.get("uid", ""),
@@ -87,6 +99,8 @@ class Reconciler:
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._strategy_next: dict[str, float] = {}
+        self._evicting: set[str] = set()  # pod uids being evicted by the controller
+        self._lost_nodes: set[str] = set()
         self.restored = 0
 
     # ------------------------------------------------------------- lifecycle
@@ -97,7 +111,7 @@ class Reconciler:
         self._threads = []
         self.restored = self.rebuild_ledger()
         for fn in (self._watch_workloads, self._watch_pods, self._watch_budgets, self._watch_strategies,
-                   self._periodic):
+                   self._watch_nodes, self._periodic):
             t = threading.Thread(target=fn, daemon=True)
             t.start()
             self._threads.append(t)
@@ -162,10 +176,11 @@ class Reconciler:
         md = gw["metadata"]
         ns, name = md.get("namespace", "default"), md["name"]
         if typ == "DELETED":
-            self.kube.delete_pod(ns, f"{name}-gw")
+            self.kube.delete_pod(ns, (gw.get("status") or {}).get("podName") or pod_name(name))
             return
         if gw.get("status", {}).get("phase") in ("Scheduling", "Scheduled", "Running", "Succeeded", "Failed"):
             return
+        restart = int((gw.get("status") or {}).get("restarts") or 0)
         gw = crds.default(gw)
         errs = crds.validate(gw)
         if errs:
@@ -185,7 +200,7 @@ class Reconciler:
                     gw["spec"]["preferredNodes"] = hint["preferred_nodes"]
             except Exception:  # noqa: BLE001 - the hint is optional
                 pass
-        pod = pod_for_workload(gw)
+        pod = pod_for_workload(gw, restart)
         try:
             self.kube.create_pod(pod)
         except ApiError as e:
@@ -209,6 +224,12 @@ class Reconciler:
         ann = md.get("annotations") or {}
         if typ == "DELETED" or phase in ("Succeeded", "Failed"):
             rel = self.p.release(uid)
+            if uid in self._evicting:  # the eviction path owns the workload's status
+                if typ == "DELETED":
+                    self._evicting.discard(uid)
+                return
+            if wl and not self._is_current_pod(ns, wl, md.get("name", "")):
+                return  # an earlier attempt's pod going away
             if wl:
                 st = {"phase": "Failed" if phase == "Failed" else "Succeeded", "completionTime": _now_iso()}
                 cost = rel.get("cost")
@@ -231,6 +252,94 @@ class Reconciler:
                   "conditions": [{"type": "Scheduled", "status": "True", "reason": "Bound",
                                   "lastTransitionTime": _now_iso()}]}
             self.kube.patch_cr_status("GPUWorkload", ns, wl, st)
+
+    def _is_current_pod(self, ns: str, wl: str, name: str) -> bool:
+        try:
+            st = self.kube.get_cr("GPUWorkload", ns, wl).get("status") or {}
+        except ApiError:
+            return True
+        return st.get("podName", name) == name
+
+    # ------------------------------------------------------------- failures
+    def _watch_nodes(self):
+        self._loop("/api/v1/nodes", self.on_node)
+
+    def on_node(self, typ: str, node: dict):
+        name = node.get("metadata", {}).get("name", "")
+        if typ == "DELETED":
+            self.evict_node(name, "node deleted")
+            self.p.remove_node(name)
+            return
+        ready = next((c.get("status") for c in (node.get("status") or {}).get("conditions") or []
+                      if c.get("type") == "Ready"), "True")
+        if ready != "True":
+            if name not in self._lost_nodes:
+                self._lost_nodes.add(name)
+                self.p.set_cordon(name, True)  # before eviction: replacements go elsewhere
+                self.evict_node(name, f"node NotReady (Ready={ready})")
+        elif name in self._lost_nodes:
+            self._lost_nodes.discard(name)
+            self.p.set_cordon(name, False)
+
+    def evict_node(self, node: str, reason: str) -> int:
+        n = 0
+        for a in self.p.allocations():
+            if a.get("node") == node:
+                self.evict(a, reason)
+                n += 1
+        return n
+
+    def health_sweep(self) -> int:
+        """Evict allocations holding a GPU (or a slice of one) that the health
+        policy marks Unhealthy."""
+        snap = self.p.snapshot().get("nodes", {})
+        n = 0
+        for a in self.p.allocations():
+            gpus = {g["uuid"]: g for g in (snap.get(a.get("node")) or {}).get("gpus", [])}
+            held = list(a.get("gpus", [])) + [p.rsplit("/p", 1)[0] for p in a.get("partitions", [])]
+            bad = [u for u in held if gpus.get(u, {}).get("health", {}).get("status") == "Unhealthy"]
+            if bad:
+                why = "; ".join(gpus[bad[0]]["health"].get("reasons") or ["unhealthy"])
+                self.evict(a, f"GPU {bad[0]} Unhealthy: {why}")
+                n += 1
+        return n
+
+    def evict(self, alloc: dict, reason: str) -> None:
+        """Release an allocation whose node or GPU failed; reschedule or fail
+        its GPUWorkload per spec.recovery."""
+        uid = alloc["uid"]
+        pod = next((p for p in self.kube.list_pods(alloc.get("namespace"))
+                    if (p["metadata"].get("uid") or "") == uid), None)
+        self._evicting.add(uid)
+        self.p.release(uid)
+        if pod is None:
+            self._evicting.discard(uid)
+            return
+        md = pod["metadata"]
+        ns = md.get("namespace", "default")
+        wl = (md.get("labels") or {}).get(LABEL_WORKLOAD)
+        self.kube.delete_pod(ns, md["name"])
+        if not wl:
+            return
+        try:
+            gw = self.kube.get_cr("GPUWorkload", ns, wl)
+        except ApiError:
+            return
+        gw = crds.default(gw)
+        rec = gw["spec"].get("recovery") or {}
+        restarts = int((gw.get("status") or {}).get("restarts") or 0)
+        cond = {"type": "Evicted", "status": "True", "reason": "NodeOrGPUFailure", "message": reason,
+                "lastTransitionTime": _now_iso()}
+        if rec.get("policy", "Reschedule") == "Reschedule" and restarts < int(rec.get("maxRestarts", 3)):
+            self.kube.patch_cr_status("GPUWorkload", ns, wl, {
+                "phase": "Pending", "restarts": restarts + 1, "lastFailure": reason,
+                "scheduledNode": "", "allocatedGPUs": [], "partitionSlices": [], "conditions": [cond]})
+            # The status watch event (phase Pending) drives on_workload: a fresh
+            # pod, which the scheduler places away from the failure.
+        else:
+            self.kube.patch_cr_status("GPUWorkload", ns, wl, {
+                "phase": "Failed", "lastFailure": reason, "restarts": restarts,
+                "message": f"evicted: {reason}", "completionTime": _now_iso(), "conditions": [cond]})
 
     # ------------------------------------------------------------- GPUBudget
     def _watch_budgets(self):
@@ -311,6 +420,7 @@ class Reconciler:
             now = time.time()
             try:
                 self.p.refresh_telemetry()
+                self.health_sweep()
                 self.p.tick(now)
                 self._rebalance_due(now)
                 self._budget_status()

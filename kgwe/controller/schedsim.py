@@ -45,6 +45,11 @@ class _Http:
         return None
 
 
+def _ready(node: dict) -> bool:
+    conds = (node.get("status") or {}).get("conditions") or []
+    return all(c.get("status") == "True" for c in conds if c.get("type") == "Ready")
+
+
 class SchedulerSim:
     def __init__(self, kube: KubeClient, extender_url: str, bind_workers: int = 4,
                  on_bound=None, on_failed=None, retry_interval_s: float = 0.05):
@@ -73,10 +78,15 @@ class SchedulerSim:
         self._stop.set()
 
     def _nodelist(self) -> list:
-        if time.time() - self._nodes_at > 5.0 or not self._nodes:
-            self._nodes = self.kube.list_nodes()
+        if time.time() - self._nodes_at > 1.0 or not self._nodes:
+            # kube-scheduler never offers a node that is not Ready (the
+            # node.kubernetes.io/not-ready taint): neither does the stand-in.
+            self._nodes = [n for n in self.kube.list_nodes() if _ready(n)]
             self._nodes_at = time.time()
         return self._nodes
+
+    def invalidate_nodes(self) -> None:
+        self._nodes_at = 0.0
 
     def _watch(self):
         rv = "0"

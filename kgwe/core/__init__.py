@@ -66,6 +66,12 @@ class Platform:
     def upsert_node(self, node: dict) -> None:
         self._p.upsert_node(json.dumps(node))
 
+    def set_cordon(self, name: str, on: bool = True) -> None:
+        self._p.set_cordon(name, on)
+
+    def cordoned(self) -> list:
+        return list(self._p.cordoned())
+
     def remove_node(self, name: str) -> None:
         self._p.remove_node(name)
 

@@ -156,6 +156,8 @@ PYBIND11_MODULE(_kgwe_core, m) {
         s.p->discovery()->upsert_node(node_from_json(Json::parse(node_json)));
       })
       .def("remove_node", [](PyPlatform& s, const std::string& n) { s.p->discovery()->remove_node(n); })
+      .def("set_cordon", [](PyPlatform& s, const std::string& n, bool on) { s.p->scheduler()->set_cordon(n, on); })
+      .def("cordoned", [](PyPlatform& s) { return s.p->scheduler()->cordoned(); })
       .def("refresh", [](PyPlatform& s) { s.p->discovery()->refresh(); },
            py::call_guard<py::gil_scoped_release>())
       .def("refresh_telemetry", [](PyPlatform& s) { s.p->discovery()->refresh_telemetry(); },

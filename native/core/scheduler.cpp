@@ -392,7 +392,22 @@ std::vector<const PartitionInstance*> Scheduler::free_partitions(
   return out;
 }
 
+void Scheduler::set_cordon(const std::string& node, bool on) {
+  std::lock_guard<std::mutex> lk(cordon_mu_);
+  if (on) cordoned_.insert(node);
+  else cordoned_.erase(node);
+}
+
+std::vector<std::string> Scheduler::cordoned() const {
+  std::lock_guard<std::mutex> lk(cordon_mu_);
+  return {cordoned_.begin(), cordoned_.end()};
+}
+
 std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w) const {
+  {
+    std::lock_guard<std::mutex> lk(cordon_mu_);
+    if (!cordoned_.empty() && cordoned_.count(n.name)) return "node cordoned (not ready)";
+  }
   if (std::find(w.exclude_nodes.begin(), w.exclude_nodes.end(), n.name) != w.exclude_nodes.end())
     return "node excluded by workload";
   for (const auto& kv : w.node_selector) {

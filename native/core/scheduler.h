@@ -202,6 +202,10 @@ class Scheduler {
   // snapshot could otherwise reserve the GPU (or a slice of it).
   bool fence_gpu(const std::string& gpu_uuid);
   void unfence_gpu(const std::string& gpu_uuid);
+  // Cordon: no new placements on the node (NotReady / draining); existing
+  // allocations are untouched.
+  void set_cordon(const std::string& node, bool on);
+  std::vector<std::string> cordoned() const;
   std::vector<Allocation> allocations() const;
   bool allocation(const std::string& uid, Allocation* out) const;
   SchedulerMetrics metrics() const;
@@ -242,6 +246,8 @@ class Scheduler {
   std::unordered_map<std::string, std::string> gpu_owner_;   // gpu uuid -> uid
   std::unordered_map<std::string, std::string> part_owner_;  // partition id -> uid
   std::set<std::string> fenced_;                             // GPUs mid partition switch
+  mutable std::mutex cordon_mu_;
+  std::set<std::string> cordoned_;
   bool gpu_has_slice_owner_locked(const std::string& gpu_uuid) const;
   std::unordered_map<std::string, int> node_gpus_used_;      // node -> allocated GPUs
   struct Gang {

@@ -292,3 +292,67 @@ def test_mixed_tenancy_training_and_partition_inference(cluster):
     for uid, a in allocs.items():
         if a["partitions"]:
             assert rates[uid] == pytest.approx(train_rate / 8, rel=0.02)
+
+
+def _status(kube, ns, name):
+    return kube.get_cr("GPUWorkload", ns, name).get("status") or {}
+
+
+def test_node_loss_reschedules_workload(cluster):
+    """the reference evicts a deleted node from its cache and
+    leaves the allocations on it stale.  Here the workload is evicted and,
+    per spec.recovery, rescheduled onto the surviving node."""
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr(gw("resilient", count=8))
+    st = wait_for(lambda: _status(kube, "ml", "resilient") if _status(kube, "ml", "resilient")
+                  .get("phase") in ("Scheduled", "Running") else None)
+    first = st["scheduledNode"]
+    kube.delete_node(first)
+    st = wait_for(lambda: _status(kube, "ml", "resilient") if _status(kube, "ml", "resilient")
+                  .get("restarts") == 1 and _status(kube, "ml", "resilient").get("phase") in
+                  ("Scheduled", "Running") else None, timeout=15)
+    assert st["scheduledNode"] != first and len(st["allocatedGPUs"]) == 8
+    assert "node deleted" in st["lastFailure"]
+    assert st["podName"] == "resilient-gw-r1"
+    allocs = plat.allocations()
+    assert len(allocs) == 1 and allocs[0]["node"] == st["scheduledNode"]
+    assert first not in plat.snapshot()["nodes"]
+
+
+def test_unhealthy_gpu_evicts_and_fail_policy(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr(gw("fragile", count=2, recovery={"policy": "Fail"}))
+    st = wait_for(lambda: _status(kube, "ml", "fragile") if _status(kube, "ml", "fragile")
+                  .get("phase") in ("Scheduled", "Running") else None)
+    bad = st["allocatedGPUs"][0]
+    plat.fake_set_health_signals(st["scheduledNode"], bad, {"ecc_uncorrectable": 3})
+    st = wait_for(lambda: _status(kube, "ml", "fragile") if _status(kube, "ml", "fragile")
+                  .get("phase") == "Failed" else None, timeout=10)
+    assert bad in st["lastFailure"] and "uncorrectable ECC" in st["lastFailure"]
+    assert not plat.allocations()
+
+
+def test_unhealthy_gpu_reschedules_away_from_it(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr(gw("healer", count=4))
+    st = wait_for(lambda: _status(kube, "ml", "healer") if _status(kube, "ml", "healer")
+                  .get("phase") in ("Scheduled", "Running") else None)
+    bad = st["allocatedGPUs"][1]
+    plat.fake_set_health_signals(st["scheduledNode"], bad, {"retired_pages": 100})
+    st = wait_for(lambda: _status(kube, "ml", "healer") if _status(kube, "ml", "healer")
+                  .get("restarts") == 1 and _status(kube, "ml", "healer").get("phase") in
+                  ("Scheduled", "Running") else None, timeout=15)
+    assert bad not in st["allocatedGPUs"] and len(st["allocatedGPUs"]) == 4
+
+
+def test_not_ready_node_evicts(cluster):
+    api, kube, plat, ext, rec = cluster
+    kube.create_cr(gw("nr", count=8))
+    st = wait_for(lambda: _status(kube, "ml", "nr") if _status(kube, "ml", "nr")
+                  .get("phase") in ("Scheduled", "Running") else None)
+    first = st["scheduledNode"]
+    kube.patch_node_status(first, {"conditions": [{"type": "Ready", "status": "False"}]})
+    st = wait_for(lambda: _status(kube, "ml", "nr") if _status(kube, "ml", "nr")
+                  .get("restarts") == 1 and _status(kube, "ml", "nr").get("phase") in
+                  ("Scheduled", "Running") else None, timeout=15)
+    assert st["scheduledNode"] != first and "NotReady" in st["lastFailure"]
