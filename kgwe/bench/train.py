@@ -17,6 +17,7 @@ import torch
 from ..models import llama
 from ..ops import FusedAdamW
 from ..parallel import dist as kdist
+from ..parallel.checkpoint import Checkpointer
 from ..parallel.fsdp import shard_model
 from ..parallel.zero import ShardedDataParallel
 from ..utils import gemm_tuning
@@ -37,6 +38,8 @@ class TrainConfig:
     parallel: str = "zero"
     data: str = "random"  # "random": fresh uniform tokens each step; "fixed": one batch
     seed: int = 1234
+    ckpt_dir: str | None = None  # sharded checkpoints (kgwe.parallel.checkpoint); resume if present
+    ckpt_every: int = 0          # steps between checkpoints (0: only at the end of run())
 
 
 _T0 = time.perf_counter()
@@ -81,6 +84,19 @@ class Trainer:
         self.tokens = torch.empty((tc.micro_batch, tc.seq_len + 1), dtype=torch.long, device=dev)
         self.tokens.random_(0, self.cfg.vocab_size, generator=self._gen)
         self.last_loss: torch.Tensor | None = None
+        self.global_step = 0
+        self.ckpt = None
+        if tc.ckpt_dir:
+            if self.dp is None:
+                raise ValueError("checkpointing needs the sharded-DP trainer (parallel='zero')")
+            self.ckpt = Checkpointer(tc.ckpt_dir)
+            got = self.ckpt.load(self.dp)
+            if got is not None:  # resumed (e.g. rescheduled after a node / GPU failure)
+                self.global_step = got["step"]
+                gs = got["extra"].get("gen_state")
+                if gs is not None and gs.numel():
+                    self._gen.set_state(gs)
+                log(info, f"resumed from {tc.ckpt_dir} at step {self.global_step}")
 
     @property
     def parallelism(self) -> str:
@@ -105,7 +121,14 @@ class Trainer:
             self.opt.step()
             self.opt.zero_grad(set_to_none=True)
         self.last_loss = loss.detach()
+        self.global_step += 1
+        if self.ckpt is not None and self.tc.ckpt_every and self.global_step % self.tc.ckpt_every == 0:
+            self.checkpoint()
         return self.last_loss
+
+    def checkpoint(self, blocking: bool = False) -> None:
+        gen = self._gen.get_state()
+        self.ckpt.save(self.dp, self.global_step, {"gen_state": gen.cpu()}, blocking=blocking)
 
     @property
     def tokens_per_step(self) -> int:
@@ -125,6 +148,41 @@ class RunResult:
     util_samples: int
     loss: float
     peak_mem_gb: float
+
+
+def train(tr: Trainer, total_steps: int) -> float:
+    """Run until ``total_steps`` (counting steps done before a resume), then
+    write a final checkpoint.  Returns the last loss."""
+    while tr.global_step < total_steps:
+        loss = tr.step()
+        if tr.global_step % 10 == 0:
+            log(tr.info, f"step {tr.global_step}: loss {loss.float().item():.4f}")
+    if tr.ckpt is not None:
+        tr.checkpoint(blocking=True)
+    return float(tr.last_loss.float().item()) if tr.last_loss is not None else float("nan")
+
+
+def main(argv=None) -> int:
+    """Training entrypoint for a placed job (``kgwe launch -- torchrun ...
+    -m kgwe.bench.train``): resumes from --ckpt-dir when a checkpoint exists."""
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="kgwe-train")
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--ckpt-dir", default=None)
+    ap.add_argument("--ckpt-every", type=int, default=0)
+    a = ap.parse_args(argv)
+    info = kdist.init(force_group=True)
+    tr = Trainer(TrainConfig(model=a.model, seq_len=a.seq_len, micro_batch=a.micro_batch, lr=a.lr,
+                             ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every), info)
+    loss = train(tr, a.steps)
+    log(info, f"done at step {tr.global_step}: loss {loss:.4f}")
+    kdist.shutdown()
+    return 0
 
 
 def timed_run(tr: Trainer, steps: int, warmup: int, sample_util: bool = True) -> RunResult:
@@ -153,3 +211,7 @@ def timed_run(tr: Trainer, steps: int, warmup: int, sample_util: bool = True) ->
             if info.device.type == "cuda" else 0.0)
     return RunResult(dt, steps, tr.tokens_per_step * steps / dt, sampler.mean,
                      len(sampler.samples), loss, peak)
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
