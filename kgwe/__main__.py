@@ -11,6 +11,7 @@ COMMANDS = {
     "agent": "kgwe.agent.agent",               # node discovery + probes + telemetry exporter (:9400)
     "optimizer": "kgwe.optimizer.server",      # gRPC :50051
     "bench-sched": "kgwe.bench.sched_latency",  # pod-create -> bind latency benchmark
+    "bench-scale": "kgwe.bench.scale",  # scheduling core on a 10k-GPU fleet
     "busbw": "kgwe.parallel.busbw",            # RCCL all-reduce bus bandwidth sweep
     "crds": "kgwe.api.crds",                   # render CRD YAML
     "launch": "kgwe.launch",                   # container entrypoint (placement env)

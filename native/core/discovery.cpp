@@ -232,10 +232,23 @@ void DiscoveryService::loop() {
 // ---------------------------------------------------------------------------
 std::vector<TopologyHint> DiscoveryService::hints(const HintRequest& req, size_t max_results) const {
   auto s = snapshot();
-  std::vector<TopologyHint> out;
+  // Pass 1: per node, the best group (greedy on a dense link table) and its
+  // score — no strings.  Pass 2 materialises only the hints returned.
+  struct Cand {
+    const NodeTopology* node;
+    std::vector<const GpuDevice*> group;
+    int score;
+    bool xgmi, one_numa;
+  };
+  std::vector<Cand> cands;
+  cands.reserve(s->nodes.size());
+  std::vector<const GpuDevice*> avail;
+  std::vector<double> bwm;
+  std::vector<int> grp;
+  std::vector<char> in;
   for (const auto& kv : s->nodes) {
     const NodeTopology& n = kv.second;
-    std::vector<const GpuDevice*> avail;
+    avail.clear();
     for (const auto& g : n.gpus) {
       if (!g.healthy()) continue;
       if (g.partition.compute != ComputePartition::SPX) {
@@ -249,61 +262,93 @@ std::vector<TopologyHint> DiscoveryService::hints(const HintRequest& req, size_t
       avail.push_back(&g);
     }
     if (static_cast<int>(avail.size()) < req.gpu_count) continue;
-    TopologyHint h;
-    h.node = n.name;
-    h.score = 50;
-    // Greedy fully-connected group, started from each GPU, best by aggregate bw.
+    const int m = static_cast<int>(avail.size());
     std::vector<const GpuDevice*> best;
-    double best_bw = -1.0;
-    for (const GpuDevice* start : avail) {
-      std::vector<const GpuDevice*> grp{start};
-      double bw = 0.0;
-      while (static_cast<int>(grp.size()) < req.gpu_count) {
-        const GpuDevice* pick = nullptr;
-        double pick_bw = -1.0;
-        for (const GpuDevice* c : avail) {
-          if (std::find(grp.begin(), grp.end(), c) != grp.end()) continue;
-          double agg = 0.0;
-          bool ok = true;
-          for (const GpuDevice* m : grp) {
-            const XgmiLink* l = c->link_to(m->uuid);
-            if (!l || !l->up || l->type != LinkType::XGMI) { ok = false; break; }
-            agg += l->effective_gbps();
-          }
-          if (ok && agg > pick_bw) { pick = c; pick_bw = agg; }
+    if (req.gpu_count > 1) {
+      bwm.assign(static_cast<size_t>(m) * m, -1.0);  // -1: no up xGMI link
+      double max_link = 0.0;
+      for (int i = 0; i < m; ++i)
+        for (const auto& l : avail[i]->links) {
+          if (!l.up || l.type != LinkType::XGMI) continue;
+          for (int j = 0; j < m; ++j)
+            if (j != i && avail[j]->uuid == l.peer_uuid) {
+              bwm[static_cast<size_t>(i) * m + j] = l.effective_gbps();
+              max_link = std::max(max_link, l.effective_gbps());
+              break;
+            }
         }
-        if (!pick) break;
-        grp.push_back(pick);
-        bw += pick_bw;
-      }
-      if (static_cast<int>(grp.size()) == req.gpu_count && bw > best_bw) {
-        best = grp;
-        best_bw = bw;
+      // Greedy fully-connected group from each start GPU, best by aggregate
+      // bandwidth; a group with every pair at the node's best link speed
+      // cannot be beaten, so the search stops there.
+      const int k = req.gpu_count;
+      const double bound = max_link * k * (k - 1) / 2.0;
+      double best_bw = -1.0;
+      in.assign(m, 0);
+      for (int start = 0; start < m && best_bw < bound - 1e-9; ++start) {
+        grp.assign(1, start);
+        std::fill(in.begin(), in.end(), 0);
+        in[start] = 1;
+        double bw = 0.0;
+        while (static_cast<int>(grp.size()) < k) {
+          int pick = -1;
+          double pick_bw = -1.0;
+          for (int c = 0; c < m; ++c) {
+            if (in[c]) continue;
+            double agg = 0.0;
+            bool ok = true;
+            const double* row = &bwm[static_cast<size_t>(c) * m];
+            for (int g : grp) {
+              if (row[g] < 0) { ok = false; break; }
+              agg += row[g];
+            }
+            if (ok && agg > pick_bw) { pick = c; pick_bw = agg; }
+          }
+          if (pick < 0) break;
+          grp.push_back(pick);
+          in[pick] = 1;
+          bw += pick_bw;
+        }
+        if (static_cast<int>(grp.size()) == k && bw > best_bw) {
+          best.clear();
+          for (int g : grp) best.push_back(avail[g]);
+          best_bw = bw;
+        }
       }
     }
-    bool xgmi_group = !best.empty() && req.gpu_count > 1;
+    Cand c{&n, {}, 50, false, false};
+    c.xgmi = !best.empty() && req.gpu_count > 1;
     if (best.empty()) best.assign(avail.begin(), avail.begin() + req.gpu_count);
-    if (xgmi_group && req.prefer_xgmi) {
-      h.score += 30;
-      h.reasons.push_back("fully connected xGMI group");
-    }
-    std::set<int> numa;
-    for (auto* g : best) numa.insert(g->numa_node);
-    if (numa.size() == 1 && req.prefer_same_numa) {
-      h.score += 10;
-      h.reasons.push_back("single NUMA domain");
-    }
-    for (auto* g : best) {
-      h.gpus.push_back(g->uuid);
-      if (!req.arch.empty() && g->arch == req.arch) h.score += 5;
-    }
+    if (c.xgmi && req.prefer_xgmi) c.score += 30;
+    c.one_numa = true;
+    for (auto* g : best) c.one_numa &= g->numa_node == best[0]->numa_node;
+    if (c.one_numa && req.prefer_same_numa) c.score += 10;
+    for (auto* g : best)
+      if (!req.arch.empty() && g->arch == req.arch) c.score += 5;
+    c.group = std::move(best);
+    cands.push_back(std::move(c));
+  }
+  auto better = [](const Cand& a, const Cand& b) {
+    return a.score != b.score ? a.score > b.score : a.node->name < b.node->name;
+  };
+  const size_t keep = max_results ? std::min(max_results, cands.size()) : cands.size();
+  std::partial_sort(cands.begin(), cands.begin() + static_cast<long>(keep), cands.end(), better);
+  std::vector<TopologyHint> out;
+  out.reserve(keep);
+  for (size_t ci = 0; ci < keep; ++ci) {
+    const Cand& c = cands[ci];
+    TopologyHint h;
+    h.node = c.node->name;
+    h.score = c.score;
+    if (c.xgmi && req.prefer_xgmi) h.reasons.push_back("fully connected xGMI group");
+    if (c.one_numa && req.prefer_same_numa) h.reasons.push_back("single NUMA domain");
+    for (auto* g : c.group) h.gpus.push_back(g->uuid);
     // Bandwidth estimate: mean pairwise effective xGMI bw, PCIe when no link.
     double sum = 0.0;
     int pairs = 0;
-    for (size_t i = 0; i < best.size(); ++i)
-      for (size_t j = i + 1; j < best.size(); ++j) {
-        const XgmiLink* l = best[i]->link_to(best[j]->uuid);
-        sum += (l && l->up) ? l->effective_gbps() : best[i]->pcie.bandwidth_gbps;
+    for (size_t i = 0; i < c.group.size(); ++i)
+      for (size_t j = i + 1; j < c.group.size(); ++j) {
+        const XgmiLink* l = c.group[i]->link_to(c.group[j]->uuid);
+        sum += (l && l->up) ? l->effective_gbps() : c.group[i]->pcie.bandwidth_gbps;
         ++pairs;
       }
     h.bandwidth_gbps = pairs ? sum / pairs : 0.0;
@@ -312,10 +357,6 @@ std::vector<TopologyHint> DiscoveryService::hints(const HintRequest& req, size_t
     else h.reasons.push_back("PCIe placement");
     out.push_back(std::move(h));
   }
-  std::sort(out.begin(), out.end(), [](const TopologyHint& a, const TopologyHint& b) {
-    return a.score != b.score ? a.score > b.score : a.node < b.node;
-  });
-  if (max_results && out.size() > max_results) out.resize(max_results);
   return out;
 }
 

@@ -511,6 +511,42 @@ int Scheduler::topology_score(const NodeTopology& n, const std::vector<const Gpu
   for (int acc = 0; acc < k && need_domains < static_cast<int>(sizes.size()); ++need_domains)
     acc += sizes[need_domains];
 
+  // Dense per-call tables, so the (up to exhaustive_limit) candidate groups
+  // are scored with array lookups only: pairwise effective bandwidth / xGMI
+  // up-ness (pair_bw resolves links by uuid), NUMA domain and PCIe switch of
+  // every free GPU as small integers.
+  std::vector<double> bwm(static_cast<size_t>(m) * m, 0.0);
+  std::vector<char> upm(static_cast<size_t>(m) * m, 0);
+  for (int i = 0; i < m; ++i)
+    for (int j = i + 1; j < m; ++j) {
+      bool up = false;
+      const double bw = pair_bw(*avail[i], *avail[j], &up);
+      bwm[i * m + j] = bwm[j * m + i] = bw;
+      upm[i * m + j] = upm[j * m + i] = up;
+    }
+  std::vector<int> dom_of(m), sw_of(m);
+  std::vector<int> dom_ids;  // numa node -> dense index
+  std::vector<std::string> sw_ids;
+  for (int i = 0; i < m; ++i) {
+    auto d = std::find(dom_ids.begin(), dom_ids.end(), avail[i]->numa_node);
+    dom_of[i] = static_cast<int>(d - dom_ids.begin());
+    if (d == dom_ids.end()) dom_ids.push_back(avail[i]->numa_node);
+    auto sw = std::find(sw_ids.begin(), sw_ids.end(), avail[i]->pcie.switch_id);
+    sw_of[i] = static_cast<int>(sw - sw_ids.begin());
+    if (sw == sw_ids.end()) sw_ids.push_back(avail[i]->pcie.switch_id);
+  }
+  const int ndom = static_cast<int>(dom_ids.size());
+  std::vector<int> dom_free(ndom), dom_total(ndom, 0);
+  for (int d = 0; d < ndom; ++d) {
+    dom_free[d] = free_numa[dom_ids[d]];
+    dom_total[d] = total_numa[dom_ids[d]];
+  }
+  // Domains with no free GPU can never become "whole free" after placement.
+  int whole_free_elsewhere = 0;
+  for (auto& kv : total_numa)
+    if (std::find(dom_ids.begin(), dom_ids.end(), kv.first) == dom_ids.end() && kv.second == 0)
+      ++whole_free_elsewhere;
+
   struct Best {
     double obj = -1e30;
     std::vector<int> idx;
@@ -519,38 +555,36 @@ int Scheduler::topology_score(const NodeTopology& n, const std::vector<const Gpu
     int domains = 0;
   } best;
   const double ideal = cfg_.rated_link_gbps * k * (k - 1) / 2.0;
-  const std::string pref_switch;
+  std::vector<int> used(ndom);
   auto evaluate = [&](const std::vector<int>& idx) {
     double agg = 0.0, minbw = 1e30;
     bool clique = true;
-    std::map<int, int> used_numa;
-    std::set<std::string> switches;
+    std::fill(used.begin(), used.end(), 0);
+    uint64_t swmask = 0;
+    bool multi_sw = false;
     for (size_t i = 0; i < idx.size(); ++i) {
-      const GpuDevice* a = avail[idx[i]];
-      used_numa[a->numa_node]++;
-      switches.insert(a->pcie.switch_id);
+      const int a = idx[i];
+      used[dom_of[a]]++;
+      if (sw_of[a] < 64) swmask |= 1ull << sw_of[a];
+      else multi_sw = true;
+      const double* row = &bwm[static_cast<size_t>(a) * m];
+      const char* urow = &upm[static_cast<size_t>(a) * m];
       for (size_t j = i + 1; j < idx.size(); ++j) {
-        bool up = false;
-        double bw = pair_bw(*a, *avail[idx[j]], &up);
-        clique &= up;
-        agg += bw;
-        minbw = std::min(minbw, bw);
+        clique &= urow[idx[j]] != 0;
+        agg += row[idx[j]];
+        minbw = std::min(minbw, row[idx[j]]);
       }
     }
-    // Domains the group spans (counted before the lookups below, which must
-    // not insert: operator[] on used_numa would add every domain as 0).
-    const int domains = static_cast<int>(used_numa.size());
-    // Fragmentation: whole NUMA domains left completely free after placement.
-    int whole_free_after = 0;
-    for (auto& kv : total_numa) {
-      auto u = used_numa.find(kv.first);
-      const int left = free_numa[kv.first] - (u == used_numa.end() ? 0 : u->second);
-      if (left == kv.second) ++whole_free_after;
+    int domains = 0, whole_free_after = whole_free_elsewhere;
+    for (int d = 0; d < ndom; ++d) {
+      domains += used[d] > 0;
+      if (dom_free[d] - used[d] == dom_total[d]) ++whole_free_after;  // domain left completely free
     }
     double obj = (clique ? 1000.0 : 0.0) + 300.0 * std::min(1.0, agg / ideal) +
                  100.0 * (need_domains > 0 ? static_cast<double>(need_domains) / domains : 1.0) +
                  20.0 * whole_free_after + 5.0 * (minbw / cfg_.rated_link_gbps);
-    if (w.topology == TopologyPreference::SamePCIeSwitch) obj += switches.size() == 1 ? 500.0 : 0.0;
+    if (w.topology == TopologyPreference::SamePCIeSwitch)
+      obj += (!multi_sw && __builtin_popcountll(swmask) == 1) ? 500.0 : 0.0;
     if (w.topology == TopologyPreference::SameNUMA) obj += domains == 1 ? 500.0 : 0.0;
     if (obj > best.obj) {
       best.obj = obj;
@@ -567,10 +601,10 @@ int Scheduler::topology_score(const NodeTopology& n, const std::vector<const Gpu
   } else {
     // Greedy clique growth from every start GPU (reference-style search,
     // but on effective bandwidth and with the same objective to pick).
-    for (int s = 0; s < m; ++s) {
-      std::vector<int> grp{s};
+    for (int s0 = 0; s0 < m; ++s0) {
+      std::vector<int> grp{s0};
       std::vector<bool> in(m, false);
-      in[s] = true;
+      in[s0] = true;
       while (static_cast<int>(grp.size()) < k) {
         int pick = -1;
         double pick_bw = -1;
@@ -579,11 +613,10 @@ int Scheduler::topology_score(const NodeTopology& n, const std::vector<const Gpu
           double aggc = 0;
           bool ok = true;
           for (int g : grp) {
-            bool up = false;
-            aggc += pair_bw(*avail[c], *avail[g], &up);
-            ok &= up;
+            aggc += bwm[static_cast<size_t>(c) * m + g];
+            ok &= upm[static_cast<size_t>(c) * m + g] != 0;
           }
-          double keyv = (ok ? 1e6 : 0) + aggc + (avail[c]->numa_node == avail[s]->numa_node ? 1 : 0);
+          double keyv = (ok ? 1e6 : 0) + aggc + (dom_of[c] == dom_of[s0] ? 1 : 0);
           if (keyv > pick_bw) {
             pick = c;
             pick_bw = keyv;

@@ -289,3 +289,14 @@ def test_group_stays_in_one_numa_domain_after_partial_use():
     alloc = next(a for a in p.allocations() if a["uid"] == "t")
     assert len({numa[u] for u in alloc["gpus"]}) == 1, alloc["gpus"]
     assert d["score"] >= 90
+
+
+def test_scale_bench_small_fleet():
+    """The 10k-GPU scale bench (kgwe bench-scale) on a 128-node fleet: every
+    op completes, and schedule / topology-query p99 stay far below the
+    85 ms SLO (PRD target for topology queries: < 10 ms)."""
+    from kgwe.bench import scale
+
+    r = scale.run(nodes=128, ops=600, live_max=300)
+    assert r["scheduled"] > 500
+    assert r["schedule_ms"]["p99"] < 40.0 and r["topology_query_ms"]["p99"] < 40.0
