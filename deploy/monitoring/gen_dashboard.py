@@ -110,6 +110,27 @@ def build() -> dict:
                    [("sum(increase(kgwe_partition_reconfigurations_total[1h])) by (result)", "{{result}}")],
                    16, y, 8, 8))
     y += 8
+    P.append(row("Health & partitions", y)); y += 1
+    P.append(panel("stat", "Unhealthy / degraded GPUs",
+                   [("count(kgwe_gpu_health_status < 1) or vector(0)", "")], 0, y, 4, 8, "short",
+                   [("green", None), ("red", 1)]))
+    P.append(panel("timeseries", "ECC errors",
+                   [("sum(kgwe_gpu_ecc_errors_total) by (node, type)", "{{node}} {{type}}")], 4, y, 7, 8))
+    P.append(panel("timeseries", "Retired HBM pages",
+                   [("sum(kgwe_gpu_retired_pages) by (node, state)", "{{node}} {{state}}")], 11, y, 7, 8))
+    P.append(panel("timeseries", "Partition slice utilization",
+                   [("kgwe_partition_instance_utilization_percent", "{{node}} {{mode}}")], 18, y, 6, 8,
+                   "percent", max_=100))
+    y += 8
+    P.append(panel("timeseries", "Active throttling",
+                   [("sum(kgwe_gpu_throttle_active) by (reason)", "{{reason}}")], 0, y, 12, 8))
+    P.append(panel("stat", "GPUs with xGMI errors",
+                   [("count(kgwe_gpu_xgmi_errors > 0) or vector(0)", "")], 12, y, 4, 8, "short",
+                   [("green", None), ("red", 1)]))
+    P.append(panel("stat", "Partition ops failed (1h)",
+                   [("sum(increase(kgwe_partition_reconfigurations_total{result=\"failed\"}[1h])) or vector(0)",
+                     "")], 16, y, 8, 8, "short", [("green", None), ("red", 1)]))
+    y += 8
     P.append(row("Cost & budget", y)); y += 1
     P.append(panel("timeseries", "GPU cost by namespace (hourly)",
                    [("sum(kgwe_gpu_cost_per_hour_dollars) by (namespace)", "{{namespace}}")], 0, y, 12, 8,
