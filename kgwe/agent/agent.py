@@ -16,8 +16,10 @@ device plugin:
   * telemetry gauges (gfx_activity = the "GPU utilization" KPI, umc
     activity, VRAM, hotspot temperature, socket power, ECC, partition mode,
     xGMI link status/bandwidth) via the core's metric registry;
-  * POST /v1/partition actuates compute/memory partition modes through
-    amd-smi (needs privileges; dry-run by default).
+  * POST /v1/partition (and gRPC SetPartition) actuates compute/memory
+    partition modes through amd-smi (needs privileges; dry-run by default);
+  * gRPC :50052 (kgwe.agent.v1.NodeAgent: GetTopology / GetTelemetry /
+    GetProbes / SetPartition, kgwe/agent/grpc_service.py).
 """
 from __future__ import annotations
 
@@ -38,6 +40,7 @@ DEFAULTS = {
     "controllerUrl": "",
     "fixture": "",
     "listen": {"host": "0.0.0.0", "port": 9400},
+    "grpc": {"enabled": True, "port": 50052},
     "intervalSeconds": 5.0,
     "probe": {"hbm": True, "xgmi": True, "bytesMB": 1024, "iters": 5, "degradedRatio": 0.7},
     "partition": {"dryRun": True},
@@ -68,9 +71,11 @@ class NodeAgent:
             node = d["node"]
         if self.probe_results:
             self._apply_probes(node)
-        self.topology = node
+        # The core's canonical form (health policy applied to the raw amd-smi
+        # / probe signals) is what the agent serves and pushes.
         self.local.upsert_node(node)
-        return node
+        self.topology = self.local.node(self.name) or node
+        return self.topology
 
     def run_probes(self) -> dict:
         """HBM self-probe per GPU; xGMI all-links probe when >= 2 GPUs."""
@@ -101,9 +106,12 @@ class NodeAgent:
                 continue
             g["hbm_measured_gbps"] = v["copy_gbps"]
             if med and v["copy_gbps"] < ratio * med:
-                g.setdefault("health", {})["status"] = "Degraded"
-                g["health"].setdefault("reasons", []).append(
-                    f"HBM copy {v['copy_gbps']:.0f} GB/s < {ratio:.0%} of node median {med:.0f}")
+                why = f"HBM copy {v['copy_gbps']:.0f} GB/s < {ratio:.0%} of node median {med:.0f}"
+                h = g.setdefault("health", {})
+                h["perf_degraded"], h["perf_reason"] = True, why  # the core's health policy input
+                if h.get("status", "Healthy") == "Healthy":
+                    h["status"] = "Degraded"
+                h.setdefault("reasons", []).append(why)
         mat = self.probe_results.get("xgmi")
         if mat:
             uuid_of = {g["index"]: g["uuid"] for g in node["gpus"]}
@@ -175,18 +183,32 @@ class NodeAgent:
                 n = int(self.headers.get("Content-Length") or 0)
                 body = json.loads(self.rfile.read(n) or b"{}")
                 if self.path.startswith("/v1/partition"):
-                    dry = body.get("dryRun", agent.cfg["partition"]["dryRun"])
-                    if dry:
-                        return self._send(200, json.dumps({"dryRun": True, "planned": body}).encode())
-                    err = core.native.amdsmi_set_partition(body["gpu"], body.get("compute", ""),
-                                                           body.get("memory", ""))
-                    return self._send(200 if not err else 409, json.dumps({"error": err}).encode())
+                    res = agent.set_partition(body)
+                    return self._send(409 if res.get("error") else 200, json.dumps(res).encode())
                 return self._send(404, b"{}")
 
         srv = ThreadingHTTPServer((self.cfg["listen"]["host"], int(self.cfg["listen"]["port"])), H)
         srv.daemon_threads = True
         threading.Thread(target=srv.serve_forever, daemon=True).start()
         return srv
+
+    def set_partition(self, body: dict) -> dict:
+        """Compute / memory partition actuation (dry-run unless configured)."""
+        if not body.get("gpu"):
+            return {"error": "gpu required"}
+        dry = body.get("dryRun", self.cfg["partition"]["dryRun"]) or self.cfg["partition"]["dryRun"]
+        if dry:
+            return {"dryRun": True, "planned": body}
+        err = core.native.amdsmi_set_partition(body["gpu"], body.get("compute", ""), body.get("memory", ""))
+        return {"error": err} if err else {"applied": body}
+
+    def serve_grpc(self):
+        from . import grpc_service
+
+        server, port = grpc_service.serve(self, int(self.cfg["grpc"]["port"]),
+                                          self.cfg["listen"]["host"])
+        self.grpc_port = port
+        return server
 
     def stop(self):
         self._stop.set()
@@ -209,7 +231,10 @@ def main(argv=None) -> int:
         print(json.dumps({"topology": agent.discover(), "probes": agent.probe_results}), flush=True)
         return 0
     agent.serve()
-    print(f"kgwe-agent {agent.name}: metrics on :{cfg['listen']['port']}", flush=True)
+    if cfg["grpc"]["enabled"]:
+        agent.serve_grpc()
+    print(f"kgwe-agent {agent.name}: metrics on :{cfg['listen']['port']}"
+          + (f", gRPC on :{agent.grpc_port}" if cfg["grpc"]["enabled"] else ""), flush=True)
     try:
         agent.loop()
     except KeyboardInterrupt:

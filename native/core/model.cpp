@@ -170,6 +170,8 @@ GpuDevice gpu_from_json(const Json& j, const std::string& node) {
   g.health.retired_pages = h.get("retired_pages").as_int(0);
   g.health.pending_retired_pages = h.get("pending_retired_pages").as_int(0);
   for (const auto& r : h.get("throttle").items()) g.health.throttle_reasons.push_back(r.str());
+  g.health.perf_degraded = h.get("perf_degraded").as_bool(false);
+  g.health.perf_reason = h.get("perf_reason").str();
   g.health.pinned = h.get("pinned").as_bool(h.get("status").is_string());
   if (!g.health.pinned) {
     int down = 0;
@@ -200,6 +202,7 @@ void apply_health_policy(Health& h, int links_down_in_topology) {
   if (h.pending_retired_pages > 0)
     degrade(std::to_string(h.pending_retired_pages) + " HBM pages pending retirement");
   if (h.xgmi_errors > 0) degrade("xGMI errors reported");
+  if (h.perf_degraded) degrade(h.perf_reason.empty() ? "probe: degraded performance" : h.perf_reason);
   const int down = h.xgmi_links_down > links_down_in_topology ? h.xgmi_links_down : links_down_in_topology;
   // A down link is excluded per link by the group search; the GPU itself
   // stays schedulable (single-GPU and partition work never crosses it).
@@ -280,6 +283,8 @@ Json to_json(const GpuDevice& g) {
   h["retired_pages"] = g.health.retired_pages;
   h["pending_retired_pages"] = g.health.pending_retired_pages;
   h["pinned"] = g.health.pinned;
+  h["perf_degraded"] = g.health.perf_degraded;
+  h["perf_reason"] = g.health.perf_reason;
   Json th = Json::array();
   for (const auto& r : g.health.throttle_reasons) th.push_back(r);
   h["throttle"] = th;

@@ -77,6 +77,10 @@ struct Health {
   int64_t retired_pages = 0;        // HBM pages retired (amdsmi_get_gpu_bad_page_info)
   int64_t pending_retired_pages = 0;  // marked bad, retired at the next reset
   std::vector<std::string> throttle_reasons;  // active violations: prochot, socket/vr/hbm thermal, ppt
+  // Measured-performance degradation reported by the node agent's probes
+  // (e.g. HBM copy rate well below the node median).
+  bool perf_degraded = false;
+  std::string perf_reason;
   bool pinned = false;              // status set by an operator / fault injection: policy leaves it
 };
 
@@ -85,7 +89,7 @@ struct Health {
 // status + reasons from the raw RAS / xGMI / throttle signals:
 //   Unhealthy: uncorrectable ECC, or retired pages >= kRetiredPageLimit
 //   Degraded : deferred ECC, correctable-ECC storm, pages pending retirement,
-//              xGMI errors
+//              xGMI errors, probe-measured performance degradation
 //   reason only: xGMI links down (the group search drops the link, not the
 //              GPU) and active throttling (prochot, PPT power, socket / VR /
 //              HBM thermal — a GPU at full load routinely sits at its cap).

@@ -74,3 +74,42 @@ def test_rccl_native_sweep_single_gpu():
     r = native_sweep(1, sizes=[1 << 20, 1 << 24], iters=5)
     assert r["ndev"] == 1 and len(r["rows"]) == 2
     assert all(row["us"] > 0 for row in r["rows"])
+
+
+def test_probe_degradation_survives_push_to_controller():
+    """A GPU the agent's HBM probe marks slow stays Degraded when the
+    controller re-derives health from the pushed signals."""
+    from kgwe.core import Platform, make_fixture
+
+    src = Platform({})
+    src.add_fake_node(make_fixture("a", 8, 2))
+    node = src.node("a")
+    node["gpus"][3]["health"].update(perf_degraded=True, perf_reason="HBM copy 3000 GB/s < 70% of median")
+    ctl = Platform({})
+    ctl.upsert_node(node)
+    h = ctl.node("a")["gpus"][3]["health"]
+    assert h["status"] == "Degraded" and any("HBM copy" in r for r in h["reasons"])
+
+
+def test_agent_grpc_service(tmp_path):
+    from kgwe.agent.grpc_service import AgentClient
+
+    fx = tmp_path / "node.json"
+    fx.write_text(json.dumps(make_fixture("n", 8, 2)))
+    cfg = load_config(DEFAULTS, sets=["nodeName=grpc-node", f"fixture={fx}", "listen.host=127.0.0.1",
+                                      "grpc.port=0"])
+    agent = NodeAgent(cfg)
+    agent.discover()
+    server = agent.serve_grpc()
+    c = AgentClient(f"127.0.0.1:{agent.grpc_port}")
+    try:
+        topo = c.call("GetTopology")
+        assert topo["node"] == "grpc-node" and len(topo["topology"]["gpus"]) == 8
+        tel = c.call("GetTelemetry")
+        assert len(tel["gpus"]) == 8 and tel["gpus"][0]["health"] == "Healthy"
+        assert c.call("SetPartition", {"gpu": tel["gpus"][0]["uuid"], "compute": "CPX"})["dryRun"] is True
+        assert "error" in c.call("SetPartition", {})
+        assert c.call("GetProbes")["probes"] == {}
+    finally:
+        c.close()
+        server.stop(0)
