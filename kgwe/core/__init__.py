@@ -151,8 +151,8 @@ class Platform:
     def strategies(self) -> list:
         return _j(self._p.strategies_json())
 
-    def ensure_partitions(self, mode: str, count: int, plan_only: bool = False) -> list:
-        return _j(self._p.ensure_partitions(mode, count, plan_only))
+    def ensure_partitions(self, mode: str, count: int, plan_only: bool = False, memory: str = "") -> list:
+        return _j(self._p.ensure_partitions(mode, count, plan_only, memory))
 
     def rebalance(self, name: str, plan_only: bool = False) -> list:
         return _j(self._p.rebalance(name, plan_only))

@@ -307,9 +307,12 @@ PYBIND11_MODULE(_kgwe_core, m) {
         return s.p->partitions()->register_strategy(strategy_from_json(Json::parse(js)));
       })
       .def("strategies_json", [](PyPlatform& s) { return list_json(s.p->partitions()->strategies()); })
-      .def("ensure_partitions", [](PyPlatform& s, const std::string& mode, int count, bool plan_only) {
-        return list_json(s.p->partitions()->ensure_capacity(compute_partition_from(mode), count, plan_only));
-      }, py::arg("mode"), py::arg("count"), py::arg("plan_only") = false)
+      .def("ensure_partitions", [](PyPlatform& s, const std::string& mode, int count, bool plan_only,
+                                   const std::string& memory) {
+        MemoryPartition m = memory_partition_from(memory.empty() ? "NPS1" : memory);
+        return list_json(s.p->partitions()->ensure_capacity(compute_partition_from(mode), count, plan_only,
+                                                            memory.empty() ? nullptr : &m));
+      }, py::arg("mode"), py::arg("count"), py::arg("plan_only") = false, py::arg("memory") = "")
       .def("rebalance", [](PyPlatform& s, const std::string& name, bool plan_only) {
         return list_json(s.p->partitions()->rebalance(name, plan_only));
       }, py::arg("name"), py::arg("plan_only") = false)

@@ -19,6 +19,13 @@ const char* to_string(OpState s) {
 // ---------------------------------------------------------------------------
 // strategies
 // ---------------------------------------------------------------------------
+bool valid_mode_combo(ComputePartition c, MemoryPartition m) {
+  if (c == ComputePartition::TPX) return false;
+  if (m == MemoryPartition::NPS1) return true;
+  if (m == MemoryPartition::NPS2) return partition_count(c) % 2 == 0;
+  return false;  // NPS4 / NPS8: not MI355X modes
+}
+
 std::string validate_strategy(const PartitionStrategy& s) {
   if (s.name.empty()) return "strategy name is required";
   if (s.distribution.empty()) return "profileDistribution must not be empty";
@@ -90,6 +97,7 @@ Json to_json(const PartitionOp& op) {
   j["gpu"] = op.gpu;
   j["from"] = to_string(op.from);
   j["to"] = to_string(op.to);
+  j["memory_to"] = to_string(op.mem_to);
   j["state"] = to_string(op.state);
   j["reason"] = op.reason;
   j["error"] = op.error;
@@ -132,11 +140,13 @@ bool PartitionController::gpu_idle(const GpuDevice& g) const {
   return g.util.gfx_activity < 5.0;
 }
 
-int PartitionController::free_slices(const ClusterTopology& c, ComputePartition mode) const {
+int PartitionController::free_slices(const ClusterTopology& c, ComputePartition mode,
+                                     const MemoryPartition* memory) const {
   int n = 0;
   for (const auto& kv : c.nodes)
     for (const auto& g : kv.second.gpus) {
       if (g.partition.compute != mode || !g.healthy() || g.partition.switching) continue;
+      if (memory && g.partition.memory != *memory) continue;
       if (sched_ && g.partition.compute == ComputePartition::SPX && sched_->gpu_busy(g)) continue;
       for (const auto& pi : g.partition.instances) {
         if (pi.in_use) continue;
@@ -155,7 +165,7 @@ int PartitionController::free_slices(const ClusterTopology& c, ComputePartition 
 
 PartitionOp PartitionController::execute(const std::string& node, const GpuDevice& g,
                                          ComputePartition to, const std::string& reason,
-                                         bool plan_only) {
+                                         bool plan_only, const MemoryPartition* mem_to) {
   PartitionOp op;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -165,7 +175,8 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
   op.gpu = g.uuid;
   op.from = g.partition.compute;
   op.to = to;
-  op.mem_to = g.partition.memory;
+  // Back to SPX always means NPS1 (SPX cannot span two memory domains).
+  op.mem_to = mem_to ? *mem_to : to == ComputePartition::SPX ? MemoryPartition::NPS1 : g.partition.memory;
   op.reason = reason;
   op.dry_run = dry_run_ || plan_only;
   op.created_ns = now_ns();
@@ -173,7 +184,10 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
     // Drain: the GPU was chosen idle; re-verify right before switching.
     op.state = OpState::Draining;
     const bool fenced = !dry_run_ && sched_;
-    if (!gpu_idle(g) || (fenced && !sched_->fence_gpu(g.uuid))) {
+    if (!valid_mode_combo(to, op.mem_to)) {
+      op.state = OpState::Failed;
+      op.error = std::string("invalid mode combination ") + to_string(to) + "/" + to_string(op.mem_to);
+    } else if (!gpu_idle(g) || (fenced && !sched_->fence_gpu(g.uuid))) {
       op.state = OpState::Failed;
       op.error = "gpu no longer idle";
     } else if (dry_run_) {
@@ -181,7 +195,15 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
     } else {
       op.state = OpState::Switching;
       auto hal = disc_->hal(node);
-      std::string err = hal ? hal->set_compute_partition(g.uuid, to) : "no HAL for node " + node;
+      // Every intermediate state must be a valid combination: towards NPS2
+      // switch compute first (X/NPS1 is always valid), towards NPS1 switch
+      // memory first.
+      std::string err = hal ? "" : "no HAL for node " + node;
+      const bool mem_change = op.mem_to != g.partition.memory;
+      const bool to_nps1 = op.mem_to == MemoryPartition::NPS1;
+      if (err.empty() && mem_change && to_nps1) err = hal->set_memory_partition(g.uuid, op.mem_to);
+      if (err.empty() && to != g.partition.compute) err = hal->set_compute_partition(g.uuid, to);
+      if (err.empty() && mem_change && !to_nps1) err = hal->set_memory_partition(g.uuid, op.mem_to);
       if (err.empty()) {
         disc_->refresh_node(node);  // re-advertise the new slices
         op.state = OpState::Completed;
@@ -200,10 +222,11 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
 }
 
 std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition mode, int count,
-                                                              bool plan_only) {
+                                                              bool plan_only, const MemoryPartition* memory) {
   std::vector<PartitionOp> out;
+  if (memory && !valid_mode_combo(mode, *memory)) return out;
   auto snap = disc_->snapshot();
-  int have = free_slices(*snap, mode);
+  int have = free_slices(*snap, mode, memory);
   if (have >= count) return out;
   const int per_gpu = partition_count(mode);
   // Candidate idle GPUs in a different mode; prefer nodes already running the
@@ -221,8 +244,10 @@ std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition m
       has_mode += g.partition.compute == mode;
       idle += gpu_idle(g);
     }
-    for (const auto& g : kv.second.gpus)
-      if (g.partition.compute != mode && gpu_idle(g)) cands.push_back({kv.first, &g, has_mode, idle});
+    for (const auto& g : kv.second.gpus) {
+      const bool wrong = g.partition.compute != mode || (memory && g.partition.memory != *memory);
+      if (wrong && gpu_idle(g)) cands.push_back({kv.first, &g, has_mode, idle});
+    }
   }
   std::stable_sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
     if (a.node_has_mode != b.node_has_mode) return a.node_has_mode > b.node_has_mode;
@@ -236,8 +261,9 @@ std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition m
     if (have >= count) break;
     PartitionOp op = execute(c.node, *c.g, mode,
                              "capacity: need " + std::to_string(count) + " " + to_string(mode) +
+                                 (memory ? std::string("/") + to_string(*memory) : std::string()) +
                                  " slices, have " + std::to_string(have),
-                             plan_only);
+                             plan_only, memory);
     out.push_back(op);
     if (op.state != OpState::Failed) have += per_gpu;
   }
@@ -295,7 +321,8 @@ std::vector<PartitionOp> PartitionController::rebalance(const std::string& name,
       }
     }
     if (target == cur) break;
-    PartitionOp op = execute(m.first, *m.second, target, "rebalance strategy " + st.name, plan_only);
+    const MemoryPartition* mem = target == ComputePartition::SPX ? nullptr : &st.memory;
+    PartitionOp op = execute(m.first, *m.second, target, "rebalance strategy " + st.name, plan_only, mem);
     out.push_back(op);
     if (op.state != OpState::Failed) {
       have[cur]--;

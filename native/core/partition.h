@@ -45,6 +45,9 @@ struct PartitionStrategy {
   int priority = 0;
 };
 
+// MI355X memory modes: NPS1 with any compute mode; NPS2 needs the compute
+// partitions to split evenly over the two memory domains (DPX / QPX / CPX).
+bool valid_mode_combo(ComputePartition c, MemoryPartition m);
 std::string validate_strategy(const PartitionStrategy& s);  // "" = valid
 PartitionStrategy strategy_from_json(const Json& j);
 Json to_json(const PartitionStrategy& s);
@@ -82,7 +85,10 @@ class PartitionController {
 
   // Plan (and unless plan_only, execute) conversions so that `count` free
   // slices of `mode` exist.  Returns the operations (possibly empty).
-  std::vector<PartitionOp> ensure_capacity(ComputePartition mode, int count, bool plan_only = false);
+  // `memory` (optional): the NPS mode the slices must have; converted GPUs
+  // are switched to it too.
+  std::vector<PartitionOp> ensure_capacity(ComputePartition mode, int count, bool plan_only = false,
+                                           const MemoryPartition* memory = nullptr);
   // Move idle GPUs toward a strategy's distribution.
   std::vector<PartitionOp> rebalance(const std::string& strategy, bool plan_only = false);
   // Return idle partitioned GPUs with no slice in use back to SPX.
@@ -100,8 +106,8 @@ class PartitionController {
  private:
   bool gpu_idle(const GpuDevice& g) const;
   PartitionOp execute(const std::string& node, const GpuDevice& g, ComputePartition to,
-                      const std::string& reason, bool plan_only);
-  int free_slices(const ClusterTopology& c, ComputePartition mode) const;
+                      const std::string& reason, bool plan_only, const MemoryPartition* mem_to = nullptr);
+  int free_slices(const ClusterTopology& c, ComputePartition mode, const MemoryPartition* memory = nullptr) const;
 
   std::shared_ptr<DiscoveryService> disc_;
   std::shared_ptr<Scheduler> sched_;

@@ -225,7 +225,8 @@ std::string Platform::filter(const std::string& body) {
   }
   auto fails = sched_->filter(w, names, &passed);
   if (passed.empty() && w.partition && cfg_.auto_provision_partitions) {
-    auto ops = part_->ensure_capacity(w.partition_mode, w.partition_count);
+    auto ops = part_->ensure_capacity(w.partition_mode, w.partition_count, false,
+                                      w.partition_memory_set ? &w.partition_memory : nullptr);
     for (const auto& op : ops)
       reg_->add("kgwe_partition_reconfigurations_total",
                 {op.node, op.state == OpState::Failed ? "failed" : "ok"}, 1);
@@ -363,7 +364,8 @@ std::string Platform::schedule(const std::string& workload_json) {
   if (w.partition && cfg_.auto_provision_partitions) {
     Decision probe = sched_->schedule(w);
     if (probe.ok) return placement_json(w, probe);
-    part_->ensure_capacity(w.partition_mode, w.partition_count);
+    part_->ensure_capacity(w.partition_mode, w.partition_count, false,
+                           w.partition_memory_set ? &w.partition_memory : nullptr);
   }
   Decision d = sched_->schedule(w);
   reg_->add("kgwe_scheduling_attempts_total", {}, 1);

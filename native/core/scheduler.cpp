@@ -149,6 +149,10 @@ WorkloadRequest workload_from_json(const Json& in) {
     w.partition = true;
     w.partition_mode = compute_partition_from(part.get("mode").str("CPX"));
     w.partition_count = static_cast<int>(part.get("count").as_int(1));
+    if (part.get("memoryMode").is_string()) {
+      w.partition_memory_set = true;
+      w.partition_memory = memory_partition_from(part.get("memoryMode").str());
+    }
   }
   const Json& mig = req.get("mig");  // legacy MIG field: map profile size to a mode
   if (!w.partition && mig.is_object()) {
@@ -207,6 +211,7 @@ Json to_json(const WorkloadRequest& w) {
   j["partition"] = w.partition;
   if (w.partition) {
     j["partition_mode"] = to_string(w.partition_mode);
+    if (w.partition_memory_set) j["partition_memory"] = to_string(w.partition_memory);
     j["partition_count"] = w.partition_count;
   }
   j["type"] = to_string(w.type);
@@ -380,6 +385,7 @@ std::vector<const PartitionInstance*> Scheduler::free_partitions(
   for (const auto& g : n.gpus) {
     if (!g.healthy() || g.partition.switching) continue;
     if (g.partition.compute != w.partition_mode) continue;
+    if (w.partition_memory_set && g.partition.memory != w.partition_memory) continue;
     if (!w.arch.empty() && g.arch != w.arch) continue;
     if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid)) continue;  // whole GPU taken / switching
     for (const auto& pi : g.partition.instances) {

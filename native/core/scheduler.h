@@ -80,6 +80,8 @@ struct WorkloadRequest {
   bool partition = false;
   ComputePartition partition_mode = ComputePartition::CPX;
   int partition_count = 0;
+  bool partition_memory_set = false;  // gpuRequirements.partition.memoryMode given
+  MemoryPartition partition_memory = MemoryPartition::NPS1;
   WorkloadType type = WorkloadType::Training;
   std::string framework = "PyTorch";
   DistributionStrategy strategy = DistributionStrategy::None;

@@ -123,3 +123,35 @@ def test_colocation_gets_disjoint_cu_masks(plat):
 def test_sharing_method_selection(plat):
     r = plat.share_allocate({"uid": "iso", "requireIsolation": True, "gpu": "GPU-n0-01"})
     assert r["method"] == "Partition"
+
+
+def test_memory_mode_requests_cpx_nps2():
+    """gpuRequirements.partition.memoryMode is honoured: a CPX/NPS2 slice
+    converts an idle GPU to CPX + NPS2 (compute first, then memory, so every
+    intermediate state is valid); a CPX/NPS1 request does not take NPS2
+    slices; SPX+NPS2 is rejected; reclaim returns the GPU to SPX/NPS1."""
+    p = Platform({})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+
+    def wl(uid, mem=None):
+        part = {"mode": "CPX", "count": 1}
+        if mem:
+            part["memoryMode"] = mem
+        return {"metadata": {"name": uid, "namespace": "inf", "uid": uid},
+                "spec": {"workloadType": "Inference", "gpuRequirements": {"count": 0, "partition": part}}}
+
+    d = p.schedule(wl("a", "NPS2"))
+    assert d["ok"]
+    g_a = d["partitions"][0].rsplit("/p", 1)[0]
+    gpu = {g["uuid"]: g for g in p.node("n0")["gpus"]}[g_a]
+    assert gpu["partition"]["compute"] == "CPX" and gpu["partition"]["memory"] == "NPS2"
+    d2 = p.schedule(wl("b", "NPS1"))
+    assert d2["ok"] and d2["partitions"][0].rsplit("/p", 1)[0] != g_a
+    d3 = p.schedule(wl("c"))  # no memory constraint: packs onto the fullest CPX GPU
+    assert d3["ok"]
+    assert p.ensure_partitions("SPX", 1, memory="NPS2") == []  # invalid combination: nothing planned
+    for u in ("a", "b", "c"):
+        p.release(u)
+    ops = p.reclaim_idle_partitions()
+    assert ops and all(o["to"] == "SPX" and o["memory_to"] == "NPS1" for o in ops)
+    assert all(g["partition"]["memory"] == "NPS1" for g in p.node("n0")["gpus"])
