@@ -325,6 +325,7 @@ NodeTopology AmdSmiHal::discover(const std::string& node_name) {
     g.index = static_cast<int>(i);
     g.node = node_name;
     amdsmi_bdf_t bdf;
+    std::memset(&bdf, 0, sizeof bdf);
     if (I.amdsmi_get_gpu_device_bdf(I.handles[i], &bdf) == AMDSMI_STATUS_SUCCESS) {
       char b[32];
       std::snprintf(b, sizeof b, "%04x:%02x:%02x.%x", static_cast<unsigned>(bdf.domain_number),
@@ -392,27 +393,39 @@ void AmdSmiHal::refresh_telemetry(NodeTopology& n) {
     if (g.index < 0 || g.index >= static_cast<int>(I.handles.size())) continue;
     auto h = I.handles[g.index];
     amdsmi_engine_usage_t eu;
+    std::memset(&eu, 0, sizeof eu);
     if (I.amdsmi_get_gpu_activity(h, &eu) == AMDSMI_STATUS_SUCCESS) {
       g.util.gfx_activity = eu.gfx_activity;
       g.util.umc_activity = eu.umc_activity;
     }
     amdsmi_vram_usage_t vu;
+    std::memset(&vu, 0, sizeof vu);
     if (I.amdsmi_get_gpu_vram_usage(h, &vu) == AMDSMI_STATUS_SUCCESS) {
       if (vu.vram_total > 0) g.memory_total_gb = vu.vram_total / 1024.0;
       g.memory_used_gb = vu.vram_used / 1024.0;
       g.util.memory_used_pct = vu.vram_total ? 100.0 * vu.vram_used / vu.vram_total : 0.0;
     }
     amdsmi_error_count_t ec;
+    std::memset(&ec, 0, sizeof ec);
     if (I.amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS) {
-      g.health.ecc_correctable = static_cast<int64_t>(ec.correctable_count);
-      g.health.ecc_uncorrectable = static_cast<int64_t>(ec.uncorrectable_count);
-      g.health.ecc_deferred = static_cast<int64_t>(ec.deferred_count);
+      // Seen on MI355X hosts without RAS access (containers): SUCCESS with
+      // the struct left as-is, i.e. uninitialised stack words (~1e14).  Any
+      // count beyond 2^40 is not a real error count: ignore the reading
+      // instead of declaring the GPU Unhealthy.
+      constexpr uint64_t kImplausible = 1ull << 40;
+      if (ec.correctable_count < kImplausible && ec.uncorrectable_count < kImplausible &&
+          ec.deferred_count < kImplausible) {
+        g.health.ecc_correctable = static_cast<int64_t>(ec.correctable_count);
+        g.health.ecc_uncorrectable = static_cast<int64_t>(ec.uncorrectable_count);
+        g.health.ecc_deferred = static_cast<int64_t>(ec.deferred_count);
+      }
     }
     int64_t temp = 0;
     if (I.amdsmi_get_temp_metric(h, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &temp) ==
         AMDSMI_STATUS_SUCCESS)
       g.util.temperature_c = static_cast<double>(temp);
     amdsmi_power_info_t pw;
+    std::memset(&pw, 0, sizeof pw);
     if (I.amdsmi_get_power_info(h, &pw) == AMDSMI_STATUS_SUCCESS)
       g.util.power_w = static_cast<double>(pw.current_socket_power ? pw.current_socket_power
                                                                    : pw.average_socket_power);

@@ -26,6 +26,8 @@ def test_amdsmi_discovery_and_health_signals():
                   "pending_retired_pages", "xgmi_errors", "xgmi_links_down", "throttle"):
             assert k in h, k
         assert h["status"] in ("Healthy", "Degraded", "Unhealthy")
+        for k in ("ecc_correctable", "ecc_uncorrectable", "ecc_deferred", "retired_pages"):
+            assert 0 <= h[k] < 2**40, (k, h[k])  # real counts, never uninitialised memory
         assert (h["status"] == "Unhealthy") == (h["ecc_uncorrectable"] > 0 or h["retired_pages"] >= 64)
     # the scheduler places onto the real node
     p = Platform({})
