@@ -208,6 +208,9 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
                                             if slice_util else None),
         "partition_slice_samples": len(slice_util),
         "topology_optimal_placements": sm.get("topology_optimal", 0),
+        # PRD KPI "preemption rate < 5 %" (docs/PRD.md:444): preemptions per bound pod
+        "preemptions": sm.get("preemptions", 0),
+        "preemption_rate_pct": round(100.0 * sm.get("preemptions", 0) / max(1, n_bound[0]), 3),
         "extender_phases_ms": ext.tracer.summary(),
         "processes": "apiserver | kube-scheduler sim | extender+core",
     }
