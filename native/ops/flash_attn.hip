@@ -1,7 +1,8 @@
 // Causal GQA flash attention for gfx950 (MI355X), bf16 in / fp32 accumulate,
 // head_dim 128, written directly on v_mfma_f32_32x32x16_bf16.
 //
-// Forward (one workgroup = 8 waves = 256 query rows of one (batch, head)):
+// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head), two
+// workgroups per CU):
 //   * each wave owns 32 query rows; Q stays in VGPRs for the whole pass
 //     (8 k-steps x bf16x8 = 32 VGPRs);
 //   * K/V tiles of 64 keys are double-buffered in LDS (K row-major with a
@@ -113,16 +114,34 @@ __device__ __forceinline__ u16x4 tr_read(const bf16_t* lds_base, int byte_off) {
   return __builtin_bit_cast(u16x4, r);
 }
 
-constexpr int BQF = 256;            // query rows per forward workgroup (8 waves x 32)
+#ifndef FA_FWD_WAVES
+#define FA_FWD_WAVES 4
+#endif
+#ifndef FA_FWD_QPW
+#define FA_FWD_QPW 1
+#endif
+constexpr int FNW = FA_FWD_WAVES;   // waves per forward workgroup
+constexpr int QPW = FA_FWD_QPW;     // 32-row query sub-blocks per wave
+constexpr int FNT = 64 * FNW;       // threads per forward workgroup
+constexpr int BQF = 32 * QPW * FNW; // query rows per forward workgroup
 constexpr int KTILE = BKV * KST;    // bf16 elements of one K buffer
 constexpr int VTILE = BKV * HD;     // bf16 elements of one V buffer
+static_assert(FNW * QPW <= 8 && 16 % FNW == 0, "at most 256 query rows, 16 staging chunks split evenly");
 
-// One workgroup = 8 waves = 256 query rows of one (batch, head); K/V tiles of
-// 64 keys double-buffered in LDS (67 KB): the global loads of tile t+1 are
-// issued before tile t's MFMAs and written to the other buffer after them, so
-// one barrier per tile separates the phases.
+// One workgroup = FNW waves x QPW 32-row sub-blocks of one (batch, head);
+// K/V tiles of 64 keys double-buffered in LDS (67 KB): the global loads of
+// tile t+1 are issued before tile t's MFMAs and written to the other buffer
+// after them, so one barrier per tile separates the phases.
+// Default geometry, measured with tools/fa_variants.hip (B=2, S=4096, causal,
+// profiles/r01_attn_counters/NOTES.md): 4 waves x 1 sub-block = 128 rows per
+// workgroup, two workgroups per CU (67 KB LDS and <= 256 VGPRs each) —
+// 641 TF/s vs 622 for 8 waves x 1 (one 512-thread workgroup per CU): the two
+// waves sharing a SIMD come from different workgroups, so their barriers do
+// not hold them in lockstep and one wave's softmax overlaps the other's
+// MFMAs.  QPW = 2 (each K / V^T fragment read feeds two MFMAs, one wave per
+// SIMD) spills past 256 arch VGPRs and runs at 400-500 TF/s.
 template <bool EVEN>
-__global__ __launch_bounds__(512) void fa_fwd_kernel(
+__global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, float* __restrict__ lse2, int S, int Hq, int Hkv, float c,
     int causal, int nQB) {
@@ -132,51 +151,57 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
   decode(nQB, Hq / Hkv, Hkv, causal, &b, &h, &hkv, &qb);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lq = lane & 31, hh = lane >> 5;
-  const int q0 = qb * BQF + w * 32;
-  const int qrow = q0 + lq;
+  const int q0 = qb * BQF + w * 32 * QPW;  // first query row of this wave
   const size_t qs = static_cast<size_t>(Hq) * HD, kvs = static_cast<size_t>(Hkv) * HD;
-  // The second-dispatched half loses VALU arbitration on every segment;
-  // one static priority bump evens it out (MI355X_MICROARCH.md, two waves/SIMD).
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  // 8 waves: the second-dispatched half loses VALU arbitration on every
+  // segment; one static priority bump evens it out (MI355X_MICROARCH.md).
+  if (FNW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 
-  bf16x8 qf[8];
-  {
+  bf16x8 qf[QPW][8];
+#pragma unroll
+  for (int j = 0; j < QPW; ++j) {
+    const int qrow = q0 + 32 * j + lq;
     const bf16_t* qp = q + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) qf[t] = (EVEN || qrow < S) ? ld16(qp + 16 * t + 8 * hh) : bf16x8{};
+    for (int t = 0; t < 8; ++t) qf[j][t] = (EVEN || qrow < S) ? ld16(qp + 16 * t + 8 * hh) : bf16x8{};
   }
-  f32x16 oacc[4];
+  f32x16 oacc[QPW][4];
+  float m[QPW], l[QPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) oacc[i] = f32x16{};
-  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < QPW; ++j) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) oacc[j][i] = f32x16{};
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
 
   const int kv_end = causal ? min(S, qb * BQF + BQF) : S;
   const int ntiles = (kv_end + BKV - 1) / BKV;
   const bf16_t* kb = k + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
   const bf16_t* vb = v + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
-  // Staging: thread t moves chunks (key, ch) = ((t + 512 i) >> 4, t & 15), i = 0, 1.
+  // Staging: thread t moves chunks (key, ch) = ((t + FNT i) >> 4, t & 15), i < NSTG.
+  constexpr int NSTG = 16 / FNW;  // 16-B chunks per thread per tile (K and V each)
   const int skey = threadIdx.x >> 4, sch = threadIdx.x & 15;
-  bf16x8 kr[2], vr[2];
-  auto gload = [&](int kt) {
+  // K and V of the next tile are staged through registers one after the
+  // other (K loaded at the top and stored after the S MFMAs, V loaded then
+  // and stored after the O MFMAs) to halve the staging registers.
+  bf16x8 sr[NSTG];
+  auto gload = [&](const bf16_t* base, int kt) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int s = kt * BKV + skey + 32 * i;
-      if (EVEN || s < S) {
-        kr[i] = ld16(kb + static_cast<size_t>(s) * kvs + sch * 8);
-        vr[i] = ld16(vb + static_cast<size_t>(s) * kvs + sch * 8);
-      } else {
-        kr[i] = bf16x8{};
-        vr[i] = bf16x8{};
-      }
+    for (int i = 0; i < NSTG; ++i) {
+      const int s = kt * BKV + skey + 4 * FNW * i;
+      sr[i] = (EVEN || s < S) ? ld16(base + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
     }
   };
-  auto swrite = [&](int buf) {
+  auto kwrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = skey + 32 * i;
-      *reinterpret_cast<bf16x8*>(&Ks[buf * KTILE + key * KST + sch * 8]) = kr[i];
-      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(&Vs[buf * VTILE]) + v_off(key, sch)) = vr[i];
-    }
+    for (int i = 0; i < NSTG; ++i)
+      *reinterpret_cast<bf16x8*>(&Ks[buf * KTILE + (skey + 4 * FNW * i) * KST + sch * 8]) = sr[i];
+  };
+  auto vwrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NSTG; ++i)
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(&Vs[buf * VTILE]) + v_off(skey + 4 * FNW * i, sch)) = sr[i];
   };
   // Transposed-read lane geometry (T10): group G = lane >> 4 reads keys
   // base + 4*(G >> 1) + qq at d chunk 4*db + 2*(G & 1) + (pp >> 1), byte 8*(pp & 1).
@@ -194,106 +219,142 @@ __global__ __launch_bounds__(512) void fa_fwd_kernel(
     for (int hi = 0; hi < 2; ++hi)
       voff[db][hi] = 256 * tr_row + tr_byte + 64 * (db ^ trq) + 16 * (tr_ch ^ (trG >> 1) ^ (2 * hi));
 
-  gload(0);
-  swrite(0);
+  gload(kb, 0);
+  kwrite(0);
+  gload(vb, 0);
+  vwrite(0);
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < ntiles) gload(kt + 1);  // lands during this tile's MFMAs
+    const bool more = kt + 1 < ntiles;
+    if (more) gload(kb, kt + 1);  // lands during this tile's S MFMAs
     const int k0 = kt * BKV;
-    if (!causal || k0 <= q0 + 31) {  // else: tile entirely above this wave's diagonal
+    const bool active = !causal || k0 <= q0 + 32 * QPW - 1;  // else: tile above this wave's diagonal
+    f32x16 sacc[QPW][2];
+    if (active) {  // else: tile entirely above this wave's diagonal
       const bf16_t* Kc = Ks + cur * KTILE;
-      const bf16_t* Vc = Vs + cur * VTILE;
-      f32x16 sacc[2] = {f32x16{}, f32x16{}};
+      // S^T = K Q^T for every sub-block: each K fragment feeds QPW MFMAs.
+#pragma unroll
+      for (int j = 0; j < QPW; ++j) sacc[j][0] = sacc[j][1] = f32x16{};
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-          sacc[st] = mfma(ld16(&Kc[(st * 32 + lq) * KST + 16 * t + 8 * hh]), qf[t], sacc[st]);
+        for (int t = 0; t < 8; ++t) {
+          const bf16x8 kf = ld16(&Kc[(st * 32 + lq) * KST + 16 * t + 8 * hh]);
+#pragma unroll
+          for (int j = 0; j < QPW; ++j) sacc[j][st] = mfma(kf, qf[j][t], sacc[j][st]);
+        }
+    }
+    // The other buffers were released by every wave at the last barrier.
+    if (more) {
+      kwrite(cur ^ 1);
+      gload(vb, kt + 1);  // lands during this tile's softmax and O MFMAs
+    }
+    if (active) {
+      const bf16_t* Vc = Vs + cur * VTILE;
       // Row max on the RAW scores (c > 0: max commutes with the scaling);
-      // the scale is folded into the exponent's FMA below.
-      float mx = -INFINITY;
+      // the scale is folded into the exponent's FMA below.  A sub-block
+      // entirely above the diagonal is masked to -inf and contributes 0.
       const bool edge = (causal && k0 + BKV - 1 > q0) || (!EVEN && k0 + BKV > S);  // wave-uniform
-      if (edge) {
+      float m_use[QPW], alpha[QPW];
+      bool moved = false;
 #pragma unroll
-        for (int st = 0; st < 2; ++st)
+      for (int j = 0; j < QPW; ++j) {
+        const int qrow = q0 + 32 * j + lq;
+        float mx = -INFINITY;
+        if (edge) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + st * 32 + acc_row(r, hh);
-            if ((!EVEN && key >= S) || (causal && key > qrow)) sacc[st][r] = -INFINITY;
-            mx = fmaxf(mx, sacc[st][r]);
-          }
-      } else {
+          for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int st = 0; st < 2; ++st)
+            for (int r = 0; r < 16; ++r) {
+              const int key = k0 + st * 32 + acc_row(r, hh);
+              if ((!EVEN && key >= S) || (causal && key > qrow)) sacc[j][st][r] = -INFINITY;
+              mx = fmaxf(mx, sacc[j][st][r]);
+            }
+        } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[st][r]);
+          for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[j][st][r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave)) * c;
+        const float m_new = fmaxf(m[j], mx);
+        m_use[j] = m_new == -INFINITY ? 0.f : m_new;
+        moved |= m_new > m[j];
+        alpha[j] = fast_exp2(m[j] - m_use[j]);
+        m[j] = m_new;
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave)) * c;
-      const float m_new = fmaxf(m, mx);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
       // Rescale O only when some row's max moved (exact; after the first few
       // tiles the running max rarely changes).
-      if (__any(m_new > m)) {
-        const float alpha = fast_exp2(m - m_use);
-        l *= alpha;
+      if (__any(moved)) {
 #pragma unroll
-        for (int db = 0; db < 4; ++db)
+        for (int j = 0; j < QPW; ++j) {
+          l[j] *= alpha[j];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-      }
-      m = m_new;
-      // P = 2^(S c - m): one FMA + one v_exp per element; the row sum is
-      // accumulated pairwise (packed adds).
-      f32x2 rs2 = {0.f, 0.f};
+          for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const float p0 = fast_exp2(fmaf(sacc[st][r], c, -m_use));
-          const float p1 = fast_exp2(fmaf(sacc[st][r + 1], c, -m_use));
-          sacc[st][r] = p0;
-          sacc[st][r + 1] = p1;
-          rs2 += f32x2{p0, p1};
+            for (int r = 0; r < 16; ++r) oacc[j][db][r] *= alpha[j];
         }
-      const float rs = rs2[0] + rs2[1];
-      l += rs + __shfl_xor(rs, 32, kWave);
+      }
+      // P = 2^(S c - m): one FMA + one v_exp per element, then bf16 pairs.
+      bf16x8 pb[QPW][4];
+#pragma unroll
+      for (int j = 0; j < QPW; ++j) {
+        float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const float p0 = fast_exp2(fmaf(sacc[j][st][r], c, -m_use[j]));
+            const float p1 = fast_exp2(fmaf(sacc[j][st][r + 1], c, -m_use[j]));
+            rs0 += p0;
+            rs1 += p1;
+            pb[j][2 * st + (r >> 3)][r & 7] = f2bf(p0);
+            pb[j][2 * st + (r >> 3)][(r & 7) + 1] = f2bf(p1);
+          }
+        const float rs = rs0 + rs1;
+        l[j] += rs + __shfl_xor(rs, 32, kWave);
+      }
       // O^T += V^T P : P (key rows, query on lane) is the B operand as is; the
       // V^T fragment (d on the lane, the permuted key order of P on k) comes
       // from two hardware-transposed reads of the row-major V tile, at the
-      // lane offsets precomputed in voff (+ a compile-time row offset).
+      // lane offsets precomputed in voff (+ a compile-time row offset); each
+      // V^T fragment feeds QPW MFMAs.
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int st = s >> 1, sp = s & 1;
-        bf16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(sacc[st][8 * sp + j]);
         const int rowc = 256 * (st * 32 + 16 * sp);
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
           const u16x4 lo = tr_read(Vc, voff[db][0] + rowc);
           const u16x4 hi = tr_read(Vc, voff[db][1] + rowc + 256 * 8);
-          oacc[db] = mfma(cat44(lo, hi), pb, oacc[db]);
+          const bf16x8 vf = cat44(lo, hi);
+#pragma unroll
+          for (int j = 0; j < QPW; ++j) oacc[j][db] = mfma(vf, pb[j][s], oacc[j][db]);
         }
       }
     }
-    if (kt + 1 < ntiles) swrite(cur ^ 1);  // the buffer every wave finished last tile
+    if (more) vwrite(cur ^ 1);
     __syncthreads();
   }
-  if (EVEN || qrow < S) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    bf16_t* op = o + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+  for (int j = 0; j < QPW; ++j) {
+    const int qrow = q0 + 32 * j + lq;
+    if (EVEN || qrow < S) {
+      const float inv = l[j] > 0.f ? 1.f / l[j] : 0.f;
+      bf16_t* op = o + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        u16x4 v4;
+      for (int db = 0; db < 4; ++db)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v4[j] = f2bf(oacc[db][4 * g4 + j] * inv);
-        *reinterpret_cast<u16x4*>(op + db * 32 + 8 * g4 + 4 * hh) = v4;
-      }
-    if (hh == 0)
-      lse2[(static_cast<size_t>(b) * Hq + h) * S + qrow] = l > 0.f ? m + log2f(l) : -INFINITY;
+        for (int g4 = 0; g4 < 4; ++g4) {
+          u16x4 v4;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) v4[jj] = f2bf(oacc[j][db][4 * g4 + jj] * inv);
+          *reinterpret_cast<u16x4*>(op + db * 32 + 8 * g4 + 4 * hh) = v4;
+        }
+      if (hh == 0)
+        lse2[(static_cast<size_t>(b) * Hq + h) * S + qrow] = l[j] > 0.f ? m[j] + log2f(l[j]) : -INFINITY;
+    }
   }
 }
 
@@ -716,12 +777,12 @@ KGWE_API int kgwe_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   if (grid > 0x7fffffff) return -1;
   const float c = scale * 1.4426950408889634f;  // softmax in the exp2 domain
   if (S % 256 == 0)
-    hipLaunchKernelGGL(fa_fwd_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(512), 0, s,
+    hipLaunchKernelGGL(fa_fwd_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(FNT), 0, s,
                        static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
                        static_cast<const bf16_t*>(v), static_cast<bf16_t*>(o), lse2, S, Hq, Hkv, c,
                        causal, nQB);
   else
-    hipLaunchKernelGGL(fa_fwd_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(512), 0, s,
+    hipLaunchKernelGGL(fa_fwd_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(FNT), 0, s,
                        static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
                        static_cast<const bf16_t*>(v), static_cast<bf16_t*>(o), lse2, S, Hq, Hkv, c,
                        causal, nQB);

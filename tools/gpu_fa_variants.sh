@@ -1,0 +1,14 @@
+#!/bin/bash
+# Run the flash-attention variant binaries built by tools/build_fa_variants.sh
+# (fa_var_bin/fa_*), base first; every variant is compared to base's dump.
+set -o pipefail
+mkdir -p gpurun_out
+out=gpurun_out/fa_variants.log
+: > $out
+timeout -k 10 60 fa_var_bin/fa_base base >> $out 2>&1 || exit $?
+for b in fa_var_bin/fa_*; do
+  t=${b##*/fa_}
+  [ "$t" = base ] && continue
+  timeout -k 10 60 $b $t /tmp/fa_base.bin >> $out 2>&1 || exit $?
+done
+cat $out
