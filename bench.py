@@ -2,28 +2,41 @@
 """Headline benchmark: avg GPU utilisation + p99 scheduling latency of an FSDP
 Llama-3-8B job on MI355X (BASELINE.json metric/config).
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-it is launched under torchrun, one rank per GPU over RCCL.  Rank 0 prints ONE
-JSON line.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` prints ONE
+JSON line.  Two ways in, one code path per rank:
 
-What is measured
-----------------
-1. Scheduling (rank 0, CPU only, before training): the job's GPUWorkload and a
-   stream of background workloads go through the real extender HTTP server
-   (filter -> prioritize -> bind, the kube-scheduler extender contract) over a
-   fake apiserver holding a mocked fleet of 8xMI355X nodes; pod-create -> bind
+* launched by torchrun (``WORLD_SIZE`` set): this process IS a rank;
+* launched bare (no ``WORLD_SIZE``; the usual ``python bench.py --gpus N``):
+  this process is only a launcher.  It never touches the GPU (no HIP call, no
+  ``import torch``): it starts ``torch.distributed.run`` with N ranks as a
+  CHILD process (one rank per GPU, RCCL over xGMI, rendezvous on 127.0.0.1),
+  forwards the ranks' logs, re-emits rank 0's JSON line and exits non-zero
+  if any rank failed.  N=1 goes through the same launcher.
+
+What each rank measures
+-----------------------
+1. Scheduling (rank 0, CPU only): the job's GPUWorkload and a stream of
+   background workloads go through the real extender HTTP server (filter ->
+   prioritize -> bind, the kube-scheduler extender contract) over a fake
+   apiserver holding a mocked fleet of 8xMI355X nodes; pod-create -> bind
    latencies feed a histogram whose p99 is reported (reference KPI:
-   docs/PRD.md:440; its in-process "P99" was a running max).
+   docs/PRD.md:440; its in-process "P99" was a running max).  It runs in a
+   child process started BEFORE the rank touches the GPU and overlaps the
+   model build / training, so the GPU does not idle behind it.
 2. Training: W untimed warmup steps, then exactly K timed steps bracketed by
    barrier + synchronize; the max wall time over ranks is used.  Each rank
-   samples amd-smi gfx_activity for its GPU during the timed steps; ``value``
-   is the mean over ranks (whole-job average GPU utilisation, %).
+   samples amd-smi gfx_activity of its GPU (a) during the K timed steps ->
+   ``value`` (mean over ranks) and (b) over the rank's whole life (model
+   build, warmup, timed steps, extra rows) -> ``util_whole_process_pct``.
+3. At N > 1 an FSDP2 row (PyTorch ``fully_shard``) is timed on the same
+   shape after the headline row (``--fsdp-row``), and the RCCL all-reduce
+   bus bandwidth over the job's own ranks is swept first.
 Synthetic tokens (a fresh uniform batch every step), random-init weights of
 the Llama-3-8B architecture, bf16 compute, fp32 master weights + AdamW step
-inside every timed step.  Data parallelism is sharded (ZeRO-2 family: the fp32
-master weights, Adam moments and reduced gradients are sharded over ranks;
-the 16 GB of bf16 weights stay replicated because 288 GB of HBM3E has room) —
-``--parallel fsdp`` runs PyTorch FSDP2 instead for comparison.
+inside every timed step.  Headline data parallelism is kgwe's sharded DP
+(ZeRO-2 = FSDP SHARD_GRAD_OP: fp32 master weights, Adam moments and reduced
+gradients sharded over ranks; the 16 GB of bf16 weights stay replicated
+because 288 GB of HBM3E has room).
 """
 from __future__ import annotations
 
@@ -37,6 +50,7 @@ BASELINE_P99_MS = 85.0    # KGWE p99 scheduling latency
 MI355X_BF16_DENSE = 2.5e15
 METRIC = ("p99 scheduling latency (ms) + avg GPU-util %, 8-GPU FSDP job on one "
           "MI355X node")
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def parse(argv=None):
@@ -50,31 +64,107 @@ def parse(argv=None):
                     help="sequences per GPU per step (4 x 4096 tokens: +7%% tok/s over 2 on "
                          "MI355X, 181 GB peak at 1 GPU; 288 GB of HBM3E has the room)")
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
-    ap.add_argument("--sched-pods", type=int, default=2000,
+    ap.add_argument("--sched-pods", type=int, default=1500,
                     help="workloads pushed through the extender for the latency p99")
+    ap.add_argument("--sched-rate", type=float, default=75.0, help="pod arrivals per second")
     ap.add_argument("--no-sched", action="store_true")
+    ap.add_argument("--no-cluster", action="store_true",
+                    help="skip the stock-kube vs kgwe cluster simulation row")
     ap.add_argument("--no-busbw", action="store_true", help="skip the RCCL all-reduce busBW probe")
     ap.add_argument("--sdpa", action="store_true", help="force PyTorch SDPA attention")
     ap.add_argument("--parallel", default="zero", choices=["zero", "fsdp"],
-                    help="zero: replicated bf16 weights + sharded fp32 optimizer/gradients "
-                         "(kgwe.parallel.zero, default); fsdp: PyTorch FSDP2")
+                    help="headline row. zero: replicated bf16 weights + sharded fp32 "
+                         "optimizer/gradients (kgwe.parallel.zero, default); fsdp: PyTorch FSDP2")
+    ap.add_argument("--fsdp-row", default="auto", choices=["auto", "on", "off"],
+                    help="also time an FSDP2 row after the headline (auto: when N > 1)")
+    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient reduce-scatter dtype of the sharded-DP path at N > 1")
+    ap.add_argument("--in-process", action="store_true",
+                    help="run as a single rank in this process (no launcher)")
     return ap.parse_args(argv)
 
 
-def run_scheduling_bench(args, world: int) -> dict | None:
-    """Runs in its own child process tree (apiserver / scheduler / extender),
-    started before this process touches the GPU."""
+# --------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv: list[str]) -> int:
+    """Parent: spawn N ranks under torch.distributed.run, never touch the GPU."""
+    import subprocess
+    import threading
+
+    n = max(1, args.gpus)
+    port = _free_port()
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["KGWE_BENCH_LAUNCHER"] = "1"
+    env.setdefault("OMP_NUM_THREADS", "4")
+    env.setdefault("PYTHONUNBUFFERED", "1")
+    print(f"[bench] launching {n} rank(s): {' '.join(cmd[2:7])} ...", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, cwd=HERE, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines: list[str] = []
+
+    def pump():
+        for ln in proc.stdout:
+            if ln.startswith('{"metric"'):
+                lines.append(ln.strip())
+            else:
+                sys.stderr.write(ln)
+                sys.stderr.flush()
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    rc = proc.wait()
+    t.join(timeout=10)
+    if rc != 0 or not lines:
+        print(f"[bench] rank launcher failed: rc={rc}, result lines={len(lines)}", file=sys.stderr)
+        return rc or 1
+    out = json.loads(lines[-1])
+    if out.get("n_gpus") != n:
+        print(f"[bench] rank 0 reported n_gpus={out.get('n_gpus')} for --gpus {n}", file=sys.stderr)
+        return 1
+    out["launcher"] = f"bench.py -> torch.distributed.run --nproc-per-node {n} (child process)"
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+# --------------------------------------------------------------------------- rank
+def start_scheduling_bench(args, world: int):
+    """Child process tree (apiserver / scheduler sim / extender), CPU only."""
     import subprocess
 
     cmd = [sys.executable, "-m", "kgwe.bench.sched_latency", "--json", "--pods",
-           str(args.sched_pods), "--job-gpus", str(world)]
+           str(args.sched_pods), "--rate", str(args.sched_rate), "--job-gpus", str(max(1, world))]
+    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=HERE)
+
+
+def start_cluster_sim():
+    import subprocess
+
+    cmd = [sys.executable, "-m", "kgwe.bench.cluster", "--json"]
+    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=HERE)
+
+
+def collect(proc, what: str, timeout: float = 400.0) -> dict | None:
+    if proc is None:
+        return None
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=400,
-                           cwd=os.path.dirname(os.path.abspath(__file__)))
-        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
-        return json.loads(line)
+        out, err = proc.communicate(timeout=timeout)
+        js = [ln for ln in out.splitlines() if ln.startswith("{")]
+        if proc.returncode != 0 or not js:
+            raise RuntimeError(f"rc={proc.returncode}: {err[-400:]}")
+        return json.loads(js[-1])
     except Exception as e:  # noqa: BLE001 - report, never fake a number
-        print(f"[bench] scheduling benchmark failed: {e}", file=sys.stderr)
+        proc.kill()
+        print(f"[bench] {what} failed: {e}", file=sys.stderr)
         return None
 
 
@@ -102,27 +192,65 @@ def meter_cost(world: int, tps: float, util: float | None) -> dict | None:
         return None
 
 
-def main(argv=None) -> int:
-    args = parse(argv)
+def _row(tr, res, args, info, kdist) -> dict:
+    """Aggregate one timed run over ranks."""
+    world = info.world_size
+    t_max = kdist.all_reduce_max(res.seconds, info)
+    got = kdist.all_gather_floats([res.util_mean if res.util_mean is not None else -1.0,
+                                   res.loss], info)
+    utils = [u[0] for u in got]
+    losses = [u[1] for u in got]
+    valid = [u for u in utils if u >= 0]
+    tps = tr.tokens_per_step * args.steps * world / t_max
+    return {"parallelism": tr.parallelism, "seconds": t_max,
+            "ms_per_step": round(1000 * t_max / args.steps, 2),
+            "util": sum(valid) / len(valid) if valid else None,
+            "util_per_rank": [round(u, 2) if u >= 0 else None for u in utils], "losses": losses,
+            "tokens_per_s": tps,
+            "mfu": tr.cfg.flops_per_token(args.seq_len) * tps / (MI355X_BF16_DENSE * world),
+            "peak_mem_gb": res.peak_mem_gb, "util_samples": res.util_samples}
+
+
+def _release_memory() -> None:
+    import gc
+
+    import torch
+
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def rank_main(args) -> int:
     import faulthandler
 
     faulthandler.dump_traceback_later(900, exit=False)  # stack dump if a phase hangs
+    rank = int(os.environ.get("RANK", "0"))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    # CPU-side benchmarks first: child processes forked before any GPU call.
+    sched_p = start_scheduling_bench(args, world_env) if rank == 0 and not args.no_sched else None
+    cluster_p = start_cluster_sim() if rank == 0 and not args.no_cluster else None
+
     import torch
 
     from kgwe.bench.train import TrainConfig, Trainer, timed_run
     from kgwe.ops import attn as attn_ops
     from kgwe.parallel import dist as kdist
+    from kgwe.utils.amdsmi_util import UtilSampler
 
     if args.sdpa:
         attn_ops.set_force_sdpa(True)
-    # Scheduling benchmark first (rank 0, CPU only, before any GPU init).
-    sched = None
-    if int(os.environ.get("RANK", "0")) == 0 and not args.no_sched:
-        sched = run_scheduling_bench(args, int(os.environ.get("WORLD_SIZE", "1")))
     info = kdist.init(force_group=True)
     world = info.world_size
-    if args.gpus != world and info.is_main:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.gpus != world:
+        if info.is_main:
+            print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        kdist.shutdown()
+        return 2
+    life = UtilSampler(info.local_rank, interval_s=0.1)
+    if info.device.type == "cuda":
+        life.start()
 
     # Reference row "142 -> 228 GB/s" (all-reduce bus bandwidth, docs/PRD.md:117-124):
     # RCCL over xGMI on this job's own ranks, before training allocates memory.
@@ -132,62 +260,93 @@ def main(argv=None) -> int:
 
         busbw = kbus.torch_sweep(sizes=[1 << 26, 1 << 28, 1 << 30], iters=10, info=info)
 
+    reduce_dtype = torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32
     tc = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
-                     activation_checkpointing=args.ckpt, parallel=args.parallel)
+                     activation_checkpointing=args.ckpt, parallel=args.parallel,
+                     reduce_dtype=reduce_dtype)
     tr = Trainer(tc, info)
-    res = timed_run(tr, args.steps, args.warmup)
+    head = _row(tr, timed_run(tr, args.steps, args.warmup), args, info, kdist)
+    attention = ("sdpa" if (args.sdpa or not attn_ops.hip_flash_available()) else "kgwe_flash_attn")
+    tuned = tr.tuned_gemms
 
-    t_max = kdist.all_reduce_max(res.seconds, info)
-    util_local = res.util_mean if res.util_mean is not None else -1.0
-    utils = [u[0] for u in kdist.all_gather_floats([util_local], info)]
-    valid = [u for u in utils if u >= 0]
-    util = sum(valid) / len(valid) if valid else None
-    tokens = tr.tokens_per_step * args.steps * world
-    tps = tokens / t_max
-    flops = tr.cfg.flops_per_token(args.seq_len) * tps
-    mfu = flops / (MI355X_BF16_DENSE * world)
+    fsdp = None
+    want_fsdp = args.fsdp_row == "on" or (args.fsdp_row == "auto" and world > 1)
+    if want_fsdp and args.parallel != "fsdp":
+        if tr.dp is not None:
+            tr.dp.close()
+        tr = None
+        _release_memory()
+        tc2 = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
+                          activation_checkpointing=args.ckpt, parallel="fsdp")
+        tr2 = Trainer(tc2, info)
+        r2 = _row(tr2, timed_run(tr2, args.steps, min(args.warmup, 3)), args, info, kdist)
+        fsdp = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r2.items()
+                if k not in ("losses", "seconds")}
+        del tr2
+    life.stop()
+    life_util = [u[0] for u in kdist.all_gather_floats(
+        [life.mean if life.mean is not None else -1.0], info)]
+    life_valid = [u for u in life_util if u >= 0]
 
     if info.is_main:
+        sched = collect(sched_p, "scheduling benchmark")
+        cluster = collect(cluster_p, "cluster simulation", timeout=120)
         p99 = sched["p99_ms"] if sched else None
-        cost = meter_cost(world, tps, util)
+        util = head["util"]
+        tps = head["tokens_per_s"]
         out = {
             "metric": METRIC,
             "value": round(util, 2) if util is not None else None,
-            "unit": "% avg gfx_activity (whole job)",
+            "unit": "% avg amd-smi gfx_activity over the K timed training steps (mean over ranks)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(1000 * t_max / args.steps, 2),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(util / BASELINE_UTIL, 4) if util is not None else None,
             "dtype": "bf16",
             "data": "synthetic tokens, random-init weights",
             "config": {"model": args.model, "global_batch": args.micro_batch * world,
-                       "seq_len": args.seq_len, "parallelism": tr.parallelism,
+                       "seq_len": args.seq_len, "parallelism": head["parallelism"],
                        "micro_batch_per_gpu": args.micro_batch,
-                       "activation_checkpointing": args.ckpt},
+                       "activation_checkpointing": args.ckpt,
+                       "grad_reduce_dtype": args.reduce_dtype if world > 1 else None},
             "p99_sched_latency_ms": round(p99, 3) if p99 is not None else None,
             "vs_baseline_p99": round(BASELINE_P99_MS / p99, 2) if p99 else None,
-            "sched": sched,
+            "util_whole_process_pct": (round(sum(life_valid) / len(life_valid), 2)
+                                       if life_valid else None),
+            "util_whole_process_note": "gfx_activity from rank start (after import) to the end "
+                                       "of the last timed row: model build, warmup, busBW sweep "
+                                       "and the FSDP row included",
             "tokens_per_s": round(tps, 1),
             "tokens_per_s_per_gpu": round(tps / world, 1),
-            "mfu_bf16_dense": round(mfu, 4),
-            "util_per_rank": [round(u, 2) for u in utils],
-            "util_samples_rank0": res.util_samples,
-            "loss": round(res.loss, 4),
-            "peak_mem_gb_rank0": round(res.peak_mem_gb, 1),
-            "attention": "sdpa" if (args.sdpa or not attn_ops.hip_flash_available())
-            else "kgwe_flash_attn",
-            "gemm_solutions": "tuned (kgwe/tuning)" if tr.tuned_gemms else "library default",
+            "mfu_bf16_dense": round(head["mfu"], 4),
+            "util_per_rank": head["util_per_rank"],
+            "util_samples_rank0": head["util_samples"],
+            "loss_per_rank": [round(x, 4) for x in head["losses"]],
+            "peak_mem_gb_rank0": round(head["peak_mem_gb"], 1),
+            "attention": attention,
+            "gemm_solutions": "tuned (kgwe/tuning)" if tuned else "library default",
+            "fsdp_row": fsdp,
             "allreduce_busbw_gbps": (round(busbw["peak_busbw_gbps"], 1) if busbw else None),
             "allreduce_sweep": busbw["rows"] if busbw else None,
-            "cost": cost,
+            "sched": sched,
+            "cluster_sim": cluster,
+            "cost": meter_cost(world, tps, util),
         }
         print(json.dumps(out), flush=True)
     kdist.barrier(info)
     kdist.shutdown()
     return 0
+
+
+def main(argv=None) -> int:
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = parse(raw)
+    if "WORLD_SIZE" not in os.environ and not args.in_process:
+        return launch(args, raw)
+    return rank_main(args)
 
 
 if __name__ == "__main__":

@@ -40,6 +40,9 @@ class TrainConfig:
     seed: int = 1234
     ckpt_dir: str | None = None  # sharded checkpoints (kgwe.parallel.checkpoint); resume if present
     ckpt_every: int = 0          # steps between checkpoints (0: only at the end of run())
+    # gradient reduce-scatter dtype of the sharded-DP path at world > 1: fp32
+    # (exact sums) or bf16 (half the xGMI bytes per step)
+    reduce_dtype: torch.dtype = torch.float32
 
 
 _T0 = time.perf_counter()
@@ -74,7 +77,7 @@ class Trainer:
         elif tc.parallel in ("zero", "none"):
             if tc.parallel == "none" and info.world_size > 1:
                 raise RuntimeError("parallel='none' with WORLD_SIZE > 1")
-            self.dp = ShardedDataParallel(self.model, lr=tc.lr)
+            self.dp = ShardedDataParallel(self.model, lr=tc.lr, reduce_dtype=tc.reduce_dtype)
             log(info, f"sharded DP over {info.world_size} rank(s): {len(self.dp.buckets)} buckets, "
                       f"replicated bf16 weights, fp32 optimizer shard "
                       f"{sum(b.shard for b in self.dp.buckets) * 12 / 2**30:.1f} GiB/rank")

@@ -39,6 +39,7 @@ class Checkpointer:
         self._thread: threading.Thread | None = None
         self._error: BaseException | None = None
         self._pending: Path | None = None  # written, not yet published
+        self._host: list[dict] | None = None  # pinned snapshot buffers, reused across saves
 
     # ------------------------------------------------------------------ save
     def save(self, dp, step: int, extra: dict | None = None, blocking: bool = False) -> Path:
@@ -56,17 +57,26 @@ class Checkpointer:
         host = []
         if stream is not None:
             stream.wait_stream(torch.cuda.current_stream(dp.device))
+        # flush() above joined the previous write, so its buffers are free again
+        reuse = self._host if self._host is not None and len(self._host) == len(state["buckets"]) \
+            and all(hb[k].shape == t.shape for hb, b in zip(self._host, state["buckets"])
+                    for k, t in b.items()) else None
         with torch.cuda.stream(stream) if stream is not None else _null():
-            for b in state["buckets"]:
+            for i, b in enumerate(state["buckets"]):
                 hb = {}
                 for k, t in b.items():
-                    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=cuda)
+                    h = reuse[i][k] if reuse is not None else torch.empty(
+                        t.shape, dtype=t.dtype, pin_memory=cuda)
                     h.copy_(t, non_blocking=cuda)
                     hb[k] = h
                 host.append(hb)
+        self._host = host
         done = torch.cuda.Event() if cuda else None
         if done is not None:
             done.record(stream)
+            # the next step's AdamW (side stream or compute stream) must not
+            # overwrite master / m / v while this copy still reads them
+            dp.fence_writes(done)
         payload = {"step": int(step), "dp_step": state["step"], "world": world, "rank": rank,
                    "numel": [b.numel for b in dp.buckets], "buckets": host, "extra": extra or {}}
         path = sdir / f"rank{rank}-of-{world}.pt"
@@ -145,6 +155,8 @@ class Checkpointer:
         saved_world = int(files[0].name.split("-of-")[1].split(".")[0])
         if saved_world == world:
             payload = torch.load(sdir / f"rank{rank}-of-{world}.pt", weights_only=True)
+            if payload["numel"] != [b.numel for b in dp.buckets]:
+                raise ValueError("checkpoint bucket layout does not match this model")
             state = {"step": payload["dp_step"], "world": world, "rank": rank,
                      "buckets": payload["buckets"]}
         else:  # elastic: re-slice every saved shard for this rank

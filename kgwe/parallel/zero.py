@@ -90,6 +90,9 @@ class ShardedDataParallel:
         self.overlap = overlap_step
         self._step = 0
         self._armed = False  # this iteration's step counter already advanced
+        # events every writer of master / m / v / flat must wait for before the
+        # next update (e.g. a checkpoint's device -> host copy still reading them)
+        self._fences: list = []
         self._plan = AdamPlan()
         params = [p for p in model.parameters() if p.requires_grad]
         if not params:
@@ -223,6 +226,8 @@ class ShardedDataParallel:
         else:
             ctx = contextlib.nullcontext()
         with ctx:
+            for ev in self._fences:
+                torch.cuda.current_stream(self.device).wait_event(ev)
             if self.world > 1:
                 b.rs_work.wait()
                 b.rs_work = None
@@ -297,6 +302,36 @@ class ShardedDataParallel:
             b.seen.clear()
             b.updated = False
         self._armed = False
+        self._fences.clear()  # every bucket's writer has waited on them
+
+    def fence_writes(self, event) -> None:
+        """The next optimizer update (every bucket, any stream) waits for
+        ``event`` before writing master / m / v / weights."""
+        if event is not None:
+            self._fences.append(event)
+
+    def close(self) -> None:
+        """Drain in-flight collectives, remove the hooks and drop the flat
+        buffers (e.g. before building another trainer in the same process)."""
+        for b in self.buckets:
+            for w in (b.rs_work, b.ag_work):
+                if w is not None:
+                    w.wait()
+            b.rs_work = b.ag_work = None
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+        for b in self.buckets:
+            for p in b.params:
+                p.grad = None
+                if hasattr(p, "_kgwe_wt"):
+                    del p._kgwe_wt
+            b.flat = b.master = b.m = b.v = b.gfull = b.gshard = b.flat_t = None
+        self.buckets = []
+        self._bucket_of.clear()
+        self._slot.clear()
 
     def zero_grad(self) -> None:
         for b in self.buckets:

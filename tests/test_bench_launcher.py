@@ -1,0 +1,69 @@
+"""bench.py as the driver runs it: ``python bench.py --gpus N`` with no
+WORLD_SIZE spawns N rank processes (torch.distributed.run, child process) and
+re-emits rank 0's JSON line.  CPU: gloo ranks on a tiny model; GPU: one rank
+through the same launcher."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(gpus: int, extra: list[str], timeout: int = 300, env_extra: dict | None = None):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    cmd = [sys.executable, "bench.py", "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
+           "--no-sched", "--no-cluster", "--no-busbw", *extra]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    return r, lines
+
+
+def test_bench_gpus2_spawns_two_gloo_ranks():
+    r, lines = _run(2, ["--model", "tiny", "--seq-len", "64", "--micro-batch", "2",
+                        "--fsdp-row", "on"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, lines  # exactly one JSON line on stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == "zero2-dp2"
+    assert out["config"]["global_batch"] == 4
+    assert "torch.distributed.run" in out["launcher"]
+    l0, l1 = out["loss_per_rank"]
+    assert l0 != l1  # the two ranks trained on different synthetic batches
+    assert out["fsdp_row"]["parallelism"] == "fsdp2"
+    assert out["fsdp_row"]["tokens_per_s"] > 0
+    assert out["tokens_per_s"] > 0 and out["ms_per_step"] > 0
+
+
+def test_bench_failing_rank_fails_the_launcher():
+    # An impossible model name makes every rank raise: the launcher must exit
+    # non-zero and print no result line.
+    r, lines = _run(2, ["--model", "no-such-model"], timeout=200)
+    assert r.returncode != 0
+    assert not any(ln.startswith('{"metric"') for ln in lines)
+
+
+def test_bench_rank_refuses_mismatched_world():
+    env = {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1"}
+    r, lines = _run(2, ["--model", "tiny", "--seq-len", "64"], env_extra=env, timeout=200)
+    assert r.returncode == 2
+    assert not any(ln.startswith('{"metric"') for ln in lines)
+
+
+@pytest.mark.gpu
+def test_bench_gpus1_through_launcher_on_gpu():
+    r, lines = _run(1, ["--model", "llama3.2-1b", "--seq-len", "2048", "--micro-batch", "2"],
+                    timeout=400)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(lines[-1])
+    assert out["n_gpus"] == 1 and "torch.distributed.run" in out["launcher"]
+    assert out["attention"] == "kgwe_flash_attn"
+    assert out["value"] is not None and out["value"] > 50.0
+    assert out["util_whole_process_pct"] is not None
