@@ -12,6 +12,8 @@ COMMANDS = {
     "optimizer": "kgwe.optimizer.server",      # gRPC :50051
     "bench-sched": "kgwe.bench.sched_latency",  # pod-create -> bind latency benchmark
     "bench-scale": "kgwe.bench.scale",  # scheduling core on a 10k-GPU fleet
+    "bench-cluster": "kgwe.bench.cluster",  # stock kube vs kgwe on one trace (simulated)
+    "bench-scaling": "kgwe.bench.scaling",  # bench.py at 1/2/4/8 GPUs -> scaling curve
     "busbw": "kgwe.parallel.busbw",            # RCCL all-reduce bus bandwidth sweep
     "crds": "kgwe.api.crds",                   # render CRD YAML
     "launch": "kgwe.launch",                   # container entrypoint (placement env)

@@ -35,7 +35,11 @@ DEFAULTS = {
     "autoProvisionPartitions": True,
     "partitionReclaimIdleSeconds": 60.0,
     "enforceBudgets": True,
-    "optimizer": {"target": ""},
+    "optimizer": {"target": "", "inProcess": True, "learn": True},
+    "partitionConsolidation": True,
+    "partitionConsolidateBelow": 0.75,
+    "partitionConsolidateAfterSeconds": 120.0,
+    "migrationCooldownSeconds": 3600.0,
     "fakeNodes": 0,
     "labelNodes": True,
     "tickSeconds": 5.0,
@@ -47,7 +51,8 @@ DEFAULTS = {
 def build(cfg: dict):
     plat = Platform({k: cfg[k] for k in ("scheduler", "cost", "partitionDryRun",
                                          "autoProvisionPartitions", "partitionReclaimIdleSeconds",
-                                         "enforceBudgets")})
+                                         "enforceBudgets", "partitionConsolidateBelow",
+                                         "partitionConsolidateAfterSeconds", "migrationCooldownSeconds")})
     for i in range(int(cfg.get("fakeNodes", 0))):
         plat.add_fake_node(make_fixture(f"mi355x-sim-{i:03d}", 8, 2))
     kube = None
@@ -77,12 +82,16 @@ def build(cfg: dict):
                          url_prefix=cfg["listen"]["urlPrefix"],
                          routes={"/v1/nodes/": agent_push, "/validate": admission, "/mutate": admission})
     optimizer = None
-    if cfg["optimizer"]["target"]:
+    if cfg["optimizer"]["target"]:  # the optimizer Deployment (gRPC :50051)
         from ..optimizer.server import OptimizerClient  # noqa: PLC0415
 
-        client = OptimizerClient(cfg["optimizer"]["target"])
-        optimizer = type("Opt", (), {"GetPlacement": lambda self, r: client.call("GetPlacement", r)})()
-    rec = Reconciler(plat, kube, optimizer=optimizer, tick_s=float(cfg["tickSeconds"])) if kube else None
+        optimizer = OptimizerClient(cfg["optimizer"]["target"])
+    elif cfg["optimizer"]["inProcess"]:
+        from ..optimizer.optimizer import OptimizerService  # noqa: PLC0415
+
+        optimizer = OptimizerService(learn=bool(cfg["optimizer"]["learn"]))
+    rec = (Reconciler(plat, kube, optimizer=optimizer, tick_s=float(cfg["tickSeconds"]),
+                      consolidate=bool(cfg["partitionConsolidation"])) if kube else None)
     return plat, ext, rec
 
 

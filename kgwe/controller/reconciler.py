@@ -21,21 +21,37 @@ which exists in the reference (D1).  Here:
   maxRestarts times), the GPUWorkload gets a fresh pod that the scheduler
   places elsewhere; status carries ``restarts`` / ``lastFailure``.
 * Restart safety (checkpoint/resume): on start the ledger is
-  rebuilt from the allocation annotations of already-bound pods, so a
-  controller restart neither leaks nor double-allocates GPUs.
+  rebuilt from the full allocation annotation of already-bound pods
+  (priority, preemptible, type, gang, share CU range included), so a
+  controller restart or leader change neither leaks GPUs nor turns a
+  non-preemptible job into a preemption victim; running cost records resume
+  from the cost journal.
+* Partition consolidation: under-used partitioned GPUs are emptied by
+  evicting their preemptible inference pods (recreated and packed onto the
+  fuller GPUs by best fit) and switched back to SPX.
+* The optimizer loop (reference WorkloadOptimizer facade,
+  src/optimizer/workload_optimizer.py:697-875, which nothing fed): per-
+  allocation amd-smi telemetry -> IngestTelemetry every tick, completion ->
+  the online model's training rows, PredictResources -> ``status.
+  recommendation`` (rightsizing: GPUs, memory, partition mode), and
+  GetPlacement with the ledger's busy GPUs over a bounded candidate set.
 """
 from __future__ import annotations
 
 import json
+import logging
 import threading
 import time
 from datetime import datetime, timezone
 
 from ..api import crds
-from ..extender.server import ANN_BW, ANN_ENV, ANN_GPUS, ANN_NODE, ANN_PARTS, ANN_SCORE
+from ..extender.server import ANN_ALLOC, ANN_BW, ANN_ENV, ANN_GPUS, ANN_NODE, ANN_PARTS, ANN_SCORE
 from .kube import ApiError, KubeClient
 from .schedsim import SCHEDULER_NAME
 
+log = logging.getLogger("kgwe.controller")
+HINT_CANDIDATE_NODES = 16  # nodes sent to GetPlacement (most free GPUs first)
+RECOMMEND_EVERY_S = 30.0
 ANN_WORKLOAD = "kgwe.amd.com/workload"
 LABEL_WORKLOAD = "kgwe.amd.com/gpuworkload"
 
@@ -91,11 +107,17 @@ def pod_for_workload(gw: dict, restart: int = 0) -> dict:
 
 
 class Reconciler:
-    def __init__(self, platform, kube: KubeClient, optimizer=None, tick_s: float = 5.0):
+    def __init__(self, platform, kube: KubeClient, optimizer=None, tick_s: float = 5.0,
+                 consolidate: bool = True):
         self.p = platform
         self.kube = kube
         self.optimizer = optimizer
         self.tick_s = tick_s
+        self.consolidate = consolidate
+        self.errors = 0                    # exceptions in the periodic loop (logged + counted)
+        self.migrations = 0
+        self._running: dict[str, tuple] = {}  # pod uid -> (ns, gpuworkload, bound at)
+        self._next_recommend = 0.0
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._strategy_next: dict[str, float] = {}
@@ -135,14 +157,24 @@ class Reconciler:
                 continue
             if pod.get("status", {}).get("phase") in ("Succeeded", "Failed"):
                 continue
-            alloc = {"uid": md.get("uid") or f"{md.get('namespace')}/{md.get('name')}", "node": node,
-                     "namespace": md.get("namespace", "default"),
-                     "team": (md.get("labels") or {}).get("kgwe.amd.com/team", ""),
-                     "gpus": [g for g in ann.get(ANN_GPUS, "").split(",") if g],
-                     "partitions": [p for p in ann.get(ANN_PARTS, "").split(",") if p],
-                     "priority": pod.get("spec", {}).get("priority", 0)}
+            uid = md.get("uid") or f"{md.get('namespace')}/{md.get('name')}"
+            try:
+                alloc = json.loads(ann[ANN_ALLOC]) if ANN_ALLOC in ann else None
+            except ValueError:
+                alloc = None
+            if alloc is None:  # pods bound by an older controller: placement only
+                alloc = {"node": node, "namespace": md.get("namespace", "default"),
+                         "team": (md.get("labels") or {}).get("kgwe.amd.com/team", ""),
+                         "gpus": [g for g in ann.get(ANN_GPUS, "").split(",") if g],
+                         "partitions": [p for p in ann.get(ANN_PARTS, "").split(",") if p],
+                         "priority": pod.get("spec", {}).get("priority", 0)}
+            alloc["uid"] = uid
+            alloc["node"] = node
             if self.p.restore_allocation(alloc):
                 n += 1
+                wl = (md.get("labels") or {}).get(LABEL_WORKLOAD)
+                if wl:
+                    self._running[uid] = (md.get("namespace", "default"), wl, time.time())
         return n
 
     def _loop(self, path: str, handler):
@@ -189,27 +221,33 @@ class Reconciler:
                 "conditions": [{"type": "Valid", "status": "False", "reason": "Invalid",
                                 "message": "; ".join(errs), "lastTransitionTime": _now_iso()}]})
             return
-        if self.optimizer is not None:  # optimizer hint -> +10 preferred-node bonus
-            try:
+        rec = None
+        if self.optimizer is not None:
+            try:  # optimizer hint -> +10 preferred-node bonus
                 req = gw["spec"]["gpuRequirements"]
-                hint = self.optimizer.GetPlacement({"workload_id": md.get("uid", name),
-                                                    "cluster_topology": self.p.snapshot(),
+                busy, cand = self._hint_view(int(req.get("count", 1) or 1))
+                hint = self.optimizer.GetPlacement({"workload_id": f"{ns}/{name}",
+                                                    "cluster_topology": cand,
                                                     "requirements": {"gpu_count": req.get("count", 1),
-                                                                     "prefer_xgmi": True}})
+                                                                     "prefer_xgmi": True,
+                                                                     "busy_gpus": busy}})
                 if hint.get("preferred_nodes"):
                     gw["spec"]["preferredNodes"] = hint["preferred_nodes"]
-            except Exception:  # noqa: BLE001 - the hint is optional
-                pass
+            except Exception as e:  # noqa: BLE001 - the hint is optional
+                log.warning("GetPlacement for %s/%s failed: %s", ns, name, e)
+            rec = self._recommend(ns, name, gw["spec"])
         pod = pod_for_workload(gw, restart)
         try:
             self.kube.create_pod(pod)
         except ApiError as e:
             if e.status != 409:
                 raise
-        self.kube.patch_cr_status("GPUWorkload", ns, name, {
-            "phase": "Scheduling", "podName": pod["metadata"]["name"],
-            "conditions": [{"type": "PodCreated", "status": "True", "reason": "Created",
-                            "lastTransitionTime": _now_iso()}]})
+        st = {"phase": "Scheduling", "podName": pod["metadata"]["name"],
+              "conditions": [{"type": "PodCreated", "status": "True", "reason": "Created",
+                              "lastTransitionTime": _now_iso()}]}
+        if rec:
+            st["recommendation"] = rec
+        self.kube.patch_cr_status("GPUWorkload", ns, name, st)
 
     # ------------------------------------------------------------- Pods
     def _watch_pods(self):
@@ -224,6 +262,13 @@ class Reconciler:
         ann = md.get("annotations") or {}
         if typ == "DELETED" or phase in ("Succeeded", "Failed"):
             rel = self.p.release(uid)
+            run = self._running.pop(uid, None)
+            if run and self.optimizer is not None and uid not in self._evicting:
+                try:  # a finished run -> a training row of the online model
+                    self.optimizer.IngestTelemetry({"workload_id": f"{run[0]}/{run[1]}", "completed": True,
+                                                    "duration_seconds": time.time() - run[2]})
+                except Exception as e:  # noqa: BLE001
+                    log.warning("optimizer completion for %s failed: %s", uid, e)
             if uid in self._evicting:  # the eviction path owns the workload's status
                 if typ == "DELETED":
                     self._evicting.discard(uid)
@@ -241,6 +286,7 @@ class Reconciler:
                     pass
             return
         if wl and pod.get("spec", {}).get("nodeName") and ANN_GPUS in ann:
+            self._running.setdefault(uid, (ns, wl, time.time()))
             st = {"phase": "Running" if phase == "Running" else "Scheduled",
                   "scheduledNode": ann.get(ANN_NODE) or pod["spec"]["nodeName"],
                   "allocatedGPUs": [g for g in ann.get(ANN_GPUS, "").split(",") if g],
@@ -304,10 +350,12 @@ class Reconciler:
                 n += 1
         return n
 
-    def evict(self, alloc: dict, reason: str) -> None:
+    def evict(self, alloc: dict, reason: str, migration: bool = False) -> None:
         """Release an allocation whose node or GPU failed; reschedule or fail
-        its GPUWorkload per spec.recovery."""
+        its GPUWorkload per spec.recovery.  migration=True (partition
+        consolidation): always reschedule, without using the recovery budget."""
         uid = alloc["uid"]
+        self._running.pop(uid, None)
         pod = next((p for p in self.kube.list_pods(alloc.get("namespace"))
                     if (p["metadata"].get("uid") or "") == uid), None)
         self._evicting.add(uid)
@@ -328,17 +376,30 @@ class Reconciler:
         gw = crds.default(gw)
         rec = gw["spec"].get("recovery") or {}
         restarts = int((gw.get("status") or {}).get("restarts") or 0)
+        if migration:
+            st = gw.get("status") or {}
+            self.kube.patch_cr_status("GPUWorkload", ns, wl, {
+                "phase": "Pending", "migrations": int(st.get("migrations") or 0) + 1,
+                "restarts": restarts + 1,  # pod name generation; recovery budget below is separate
+                "recoveryRestarts": int(st.get("recoveryRestarts", restarts) or 0),
+                "scheduledNode": "", "allocatedGPUs": [], "partitionSlices": [],
+                "conditions": [{"type": "Migrated", "status": "True", "reason": "PartitionConsolidation",
+                                "message": reason, "lastTransitionTime": _now_iso()}]})
+            return
+        gen = restarts
+        restarts = int((gw.get("status") or {}).get("recoveryRestarts", restarts) or 0)
         cond = {"type": "Evicted", "status": "True", "reason": "NodeOrGPUFailure", "message": reason,
                 "lastTransitionTime": _now_iso()}
         if rec.get("policy", "Reschedule") == "Reschedule" and restarts < int(rec.get("maxRestarts", 3)):
             self.kube.patch_cr_status("GPUWorkload", ns, wl, {
-                "phase": "Pending", "restarts": restarts + 1, "lastFailure": reason,
+                "phase": "Pending", "restarts": gen + 1, "recoveryRestarts": restarts + 1,
+                "lastFailure": reason,
                 "scheduledNode": "", "allocatedGPUs": [], "partitionSlices": [], "conditions": [cond]})
             # The status watch event (phase Pending) drives on_workload: a fresh
             # pod, which the scheduler places away from the failure.
         else:
             self.kube.patch_cr_status("GPUWorkload", ns, wl, {
-                "phase": "Failed", "lastFailure": reason, "restarts": restarts,
+                "phase": "Failed", "lastFailure": reason, "restarts": gen, "recoveryRestarts": restarts,
                 "message": f"evicted: {reason}", "completionTime": _now_iso(), "conditions": [cond]})
 
     # ------------------------------------------------------------- GPUBudget
@@ -417,12 +478,111 @@ class Reconciler:
     # ------------------------------------------------------------- periodic
     def _periodic(self):
         while not self._stop.wait(self.tick_s):
-            now = time.time()
+            self.tick_once(time.time())
+
+    def tick_once(self, now: float) -> None:
+        # Each step fails on its own: one broken step neither hides the error
+        # nor starves the others.  Errors are logged and counted
+        # (kgwe_controller_errors_total on /metrics via the platform).
+        for name, step in (("telemetry", self.p.refresh_telemetry), ("health", self.health_sweep),
+                           ("tick", lambda: self.p.tick(now)), ("rebalance", lambda: self._rebalance_due(now)),
+                           ("consolidate", lambda: self._consolidate(now)),
+                           ("optimizer", lambda: self._feed_optimizer(now)),
+                           ("budgets", self._budget_status)):
             try:
-                self.p.refresh_telemetry()
-                self.health_sweep()
-                self.p.tick(now)
-                self._rebalance_due(now)
-                self._budget_status()
-            except Exception:  # noqa: BLE001
-                pass
+                step()
+            except Exception as e:  # noqa: BLE001
+                self.errors += 1
+                log.exception("controller %s step failed: %s", name, e)
+                try:
+                    self.p.count_error(name)
+                except Exception:  # noqa: BLE001
+                    pass
+
+    # ------------------------------------------------------------- consolidation
+    def _consolidate(self, now: float) -> None:
+        if not self.consolidate:
+            return
+        for m in self.p.consolidate_partitions(now, plan_only=True):
+            alloc = next((a for a in self.p.allocations() if a["uid"] == m["uid"]), None)
+            if alloc is None:
+                continue
+            self.migrations += 1
+            self.evict(alloc, f"partition consolidation: {m['from']} -> a fuller GPU", migration=True)
+
+    # ------------------------------------------------------------- optimizer loop
+    def _hint_view(self, k: int) -> tuple[list, dict]:
+        """(busy GPU uuids, snapshot restricted to the nodes with the most free
+        GPUs) — GetPlacement sees the ledger and a bounded candidate set, not
+        the whole fleet per workload."""
+        snap = self.p.snapshot()
+        busy = set()
+        for a in self.p.allocations():
+            busy.update(a.get("gpus", []))
+            if a.get("shared_gpu"):
+                busy.add(a["shared_gpu"])
+            busy.update(p.rsplit("/p", 1)[0] for p in a.get("partitions", []))
+        nodes = snap.get("nodes", {})
+        free = {n: sum(1 for g in v["gpus"] if g["uuid"] not in busy) for n, v in nodes.items()}
+        keep = sorted((n for n in nodes if free[n] >= k), key=lambda n: (-free[n], n))[:HINT_CANDIDATE_NODES]
+        return sorted(busy), {"nodes": {n: nodes[n] for n in keep}}
+
+    def _recommend(self, ns: str, name: str, spec: dict) -> dict | None:
+        try:
+            hints = {"workload_type": spec.get("workloadType", "Training"),
+                     "framework": spec.get("framework"),
+                     "strategy": (spec.get("distributedConfig") or {}).get("strategy")}
+            if spec.get("modelParamsBillions") is not None:
+                hints["model_params_billions"] = float(spec["modelParamsBillions"])
+            pr = self.optimizer.PredictResources({"workload_id": f"{ns}/{name}", "hints": hints})
+        except Exception as e:  # noqa: BLE001
+            log.warning("PredictResources for %s/%s failed: %s", ns, name, e)
+            return None
+        if not pr or pr.get("error"):
+            return None
+        return {"gpus": pr.get("recommended_gpus"), "memoryGB": pr.get("recommended_memory_gb"),
+                "partition": pr.get("recommended_partition"),
+                "expectedUtilization": round(float(pr.get("expected_utilization") or 0.0), 1),
+                "confidence": round(float(pr.get("confidence") or 0.0), 3),
+                "costPerHour": round(float(pr.get("estimated_cost_per_hour") or 0.0), 3),
+                "reasoning": pr.get("reasoning", [])[-3:], "updated": _now_iso()}
+
+    def _feed_optimizer(self, now: float) -> None:
+        if self.optimizer is None or not self._running:
+            return
+        gpus = {g["uuid"]: g for n in self.p.snapshot().get("nodes", {}).values() for g in n["gpus"]}
+        for a in self.p.allocations():
+            run = self._running.get(a["uid"])
+            if run is None:
+                continue
+            held = list(a.get("gpus", [])) + ([a["shared_gpu"]] if a.get("shared_gpu") else []) + \
+                [p.rsplit("/p", 1)[0] for p in a.get("partitions", [])]
+            samples = []
+            for u in held:
+                g = gpus.get(u)
+                if g is None:
+                    continue
+                samples.append({"timestamp": now, "gpu_uuid": u,
+                                "gpu_utilization": float(g["util"]["gfx_activity"]),
+                                "memory_used_bytes": int(g["memory_used_gb"] * 2**30),
+                                "memory_total_bytes": int(max(1.0, g["memory_total_gb"]) * 2**30),
+                                "power_watts": float(g["util"]["power_w"]),
+                                "temperature_celsius": float(g["util"]["temperature_c"])})
+            if samples:
+                # one sample per allocation per tick: the mean over its GPUs
+                n = len(samples)
+                agg = dict(samples[0])
+                for k in ("gpu_utilization", "power_watts", "temperature_celsius"):
+                    agg[k] = sum(x[k] for x in samples) / n
+                agg["memory_used_bytes"] = sum(x["memory_used_bytes"] for x in samples) // n
+                self.optimizer.IngestTelemetry({"workload_id": f"{run[0]}/{run[1]}", "samples": [agg]})
+        if now >= self._next_recommend:
+            self._next_recommend = now + RECOMMEND_EVERY_S
+            for uid, (ns, wl, _) in list(self._running.items()):
+                try:
+                    gw = self.kube.get_cr("GPUWorkload", ns, wl)
+                except ApiError:
+                    continue
+                rec = self._recommend(ns, wl, gw.get("spec") or {})
+                if rec:
+                    self.kube.patch_cr_status("GPUWorkload", ns, wl, {"recommendation": rec})

@@ -160,6 +160,31 @@ class Platform:
     def reclaim_idle_partitions(self, plan_only: bool = False) -> list:
         return _j(self._p.reclaim_idle_partitions(plan_only))
 
+    def reclaim_idle_after(self, now: float, min_idle_s: float) -> list:
+        """Partitioned GPUs idle for >= min_idle_s go back to SPX (the tick's
+        hysteresis reclaim, with an explicit clock — simulations)."""
+        return _j(self._p.reclaim_idle_after(now, min_idle_s))
+
+    def consolidate_partitions(self, now: float | None = None, plan_only: bool = True) -> list:
+        """Consolidating rebalance of partitioned GPUs: list of slice moves
+        {uid, from, to, node_from, node_to}.  plan_only=True (controller): the
+        caller evicts the moved pods; False: the ledger moves them itself."""
+        return _j(self._p.consolidate_partitions(time.time() if now is None else now, plan_only))
+
+    def pod_latency_quantile_ms(self, q: float) -> float:
+        """Pod create -> bind latency quantile recorded by bind() itself."""
+        return self._p.pod_latency_quantile_ms(q)
+
+    def pod_latency_count(self) -> int:
+        return self._p.pod_latency_count()
+
+    def queue_depth(self) -> int:
+        return self._p.queue_depth()
+
+    def count_error(self, step: str) -> None:
+        """kgwe_controller_errors_total{step}."""
+        self._p.count_error(step)
+
     def partition_ops(self) -> list:
         return _j(self._p.partition_ops_json())
 
@@ -220,6 +245,10 @@ class Platform:
 
     def set_pricing(self, p: dict) -> None:
         self._p.set_pricing(json.dumps(p))
+
+    def cost_resumed(self) -> int:
+        """Running usage records restored from the journal (failover)."""
+        return self._p.cost_resumed()
 
     def cost_replayed(self) -> int:
         return self._p.cost_replayed()

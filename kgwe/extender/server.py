@@ -15,14 +15,14 @@ On a successful bind the shell also:
     kgwe.amd.com/rccl-env, ...) — consumed at container start by
     ``kgwe.launch`` (downward API) to export HIP_VISIBLE_DEVICES and the RCCL
     rank environment;
-  * records the pod-create -> bind latency into the p99 histogram.
+  * (inside the C++ bind) records the pod-create -> bind latency into the
+    p99 histogram, from the webhook's microsecond admission stamp or the
+    pod's first filter call.
 """
 from __future__ import annotations
 
 import json
 import threading
-import time
-from datetime import datetime, timezone
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 from ..core import Platform
@@ -34,16 +34,25 @@ ANN_ENV = "kgwe.amd.com/rccl-env"
 ANN_NODE = "kgwe.amd.com/node"
 ANN_SCORE = "kgwe.amd.com/score"
 ANN_BW = "kgwe.amd.com/estimated-bandwidth-gbps"
+# The full ledger entry (scheduling semantics included: priority,
+# preemptible, type, gang, share CU range) — what a new leader restores.
+ANN_ALLOC = "kgwe.amd.com/allocation"
 
 
-def _created_s(meta: dict) -> float | None:
-    ts = meta.get("creationTimestamp")
-    if not ts:
-        return None
-    try:
-        return datetime.strptime(ts, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=timezone.utc).timestamp()
-    except ValueError:
-        return None
+def allocation_record(pl: dict) -> dict:
+    """Ledger entry of a bind placement, in the form
+    ``Platform.restore_allocation`` takes back."""
+    w = pl.get("workload") or {}
+    rec = {"uid": pl.get("uid", ""), "node": pl.get("node", ""), "gpus": pl.get("gpus", []),
+           "partitions": pl.get("partitions", []), "namespace": w.get("namespace", "default"),
+           "team": w.get("team", ""), "type": w.get("type", "Training"),
+           "priority": w.get("priority", 0), "preemptible": w.get("preemptible", True),
+           "gang": w.get("gang", ""), "gang_size": w.get("gang_size", 0),
+           "bandwidth_gbps": pl.get("bandwidth_gbps", 0.0)}
+    if pl.get("sharing"):
+        rec.update({k: pl[k] for k in ("sharing", "shared_gpu", "cu_begin", "cu_end", "share_memory_gb")
+                    if k in pl})
+    return rec
 
 
 class ExtenderServer:
@@ -184,20 +193,17 @@ class ExtenderServer:
             return result
         pl = res["placement"]
         if self.kube is not None:
-            ann = {ANN_GPUS: ",".join(pl.get("gpus", [])), ANN_PARTS: ",".join(pl.get("partitions", [])),
+            ann = {ANN_GPUS: ",".join(pl.get("gpus", []) or ([pl["shared_gpu"]] if pl.get("shared_gpu") else [])),
+                   ANN_PARTS: ",".join(pl.get("partitions", [])),
                    ANN_ENV: json.dumps(pl.get("env", {}), sort_keys=True), ANN_NODE: node,
-                   ANN_SCORE: str(pl.get("score", 0)), ANN_BW: f"{pl.get('bandwidth_gbps', 0.0):.1f}"}
+                   ANN_SCORE: str(pl.get("score", 0)), ANN_BW: f"{pl.get('bandwidth_gbps', 0.0):.1f}",
+                   ANN_ALLOC: json.dumps(allocation_record(pl), sort_keys=True)}
             try:
                 self.kube.patch_pod(ns, name, {"metadata": {"annotations": ann}})
                 self.kube.bind_pod(ns, name, node, uid)
             except Exception as e:  # noqa: BLE001
                 self.platform.release(pl.get("uid") or uid)
                 return {"error": f"binding failed: {e}"}
-            if pod is None:
-                pod = {"metadata": {}}
-            created = _created_s(pod.get("metadata", {}))
-            if created is not None:
-                self.platform.observe_pod_latency_ms(max(0.0, (time.time() - created) * 1000.0))
         return {}
 
     def start(self) -> "ExtenderServer":

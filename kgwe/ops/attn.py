@@ -3,7 +3,8 @@
 Dispatch order on a GPU:
   1. ``kgwe_flash_attn_*`` — the hand-written gfx950 MFMA flash-attention
      kernels in ``native/ops/flash_attn.hip`` (when built into the library);
-  2. otherwise PyTorch SDPA (ROCm flash backend) with the GQA heads expanded.
+  2. otherwise (head_dim != 128, or forced) PyTorch SDPA (ROCm flash
+     backend) with the GQA heads expanded.
 On CPU the fp32 reference is used.
 """
 from __future__ import annotations
@@ -79,7 +80,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = 
     """q [B,S,Hq,D], k/v [B,S,Hkv,D] -> o [B,S,Hq,D]."""
     if not use_hip(q):
         return ref.attention(q, k, v, causal)
-    if not _FORCE_SDPA and hip_flash_available():
+    if not _FORCE_SDPA and q.shape[-1] == 128 and hip_flash_available():
         return _FlashAttn.apply(q.contiguous(), k.contiguous(), v.contiguous(), causal)
     hq, hkv = q.shape[2], k.shape[2]
     qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)

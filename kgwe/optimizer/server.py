@@ -52,6 +52,19 @@ class OptimizerClient:
     def call(self, method: str, request: dict | None = None) -> dict:
         return self._stubs[method](request or {}, timeout=self.timeout)
 
+    # Same surface as OptimizerService, so the controller takes either.
+    def PredictResources(self, request: dict) -> dict:  # noqa: N802
+        return self.call("PredictResources", request)
+
+    def GetPlacement(self, request: dict) -> dict:  # noqa: N802
+        return self.call("GetPlacement", request)
+
+    def IngestTelemetry(self, request: dict) -> dict:  # noqa: N802
+        return self.call("IngestTelemetry", request)
+
+    def GetMetrics(self, request: dict | None = None) -> dict:  # noqa: N802
+        return self.call("GetMetrics", request)
+
     def close(self):
         self.channel.close()
 

@@ -32,6 +32,7 @@ PlatformConfig config_from_json(const std::string& s) {
   c.sched.pack = sc.get("placement").str("pack") != "spread";
   const Json& cc = j.get("cost");
   c.cost.journal_path = cc.get("journalPath").str();
+  c.cost.journal_interval_s = cc.get("journalIntervalSeconds").as_number(c.cost.journal_interval_s);
   c.cost.enable_spot = cc.get("enableSpotOptimization").as_bool(true);
   c.cost.enable_rightsizing = cc.get("enableRightsizing").as_bool(true);
   c.partition_dry_run = j.get("partitionDryRun").as_bool(false);
@@ -40,6 +41,11 @@ PlatformConfig config_from_json(const std::string& s) {
   c.enforce_budgets = j.get("enforceBudgets").as_bool(true);
   c.master_port = static_cast<int>(j.get("masterPort").as_int(29500));
   c.gpu_resource = j.get("gpuResource").str("amd.com/gpu");
+  c.consolidate.below = j.get("partitionConsolidateBelow").as_number(c.consolidate.below);
+  c.consolidate.after_s = j.get("partitionConsolidateAfterSeconds").as_number(c.consolidate.after_s);
+  c.consolidate.cooldown_s = j.get("migrationCooldownSeconds").as_number(c.consolidate.cooldown_s);
+  c.sched.max_share_clients = static_cast<int>(sc.get("maxShareClients").as_int(c.sched.max_share_clients));
+  c.sched.default_cu_percent = sc.get("defaultCuPercent").as_number(c.sched.default_cu_percent);
   return c;
 }
 
@@ -67,6 +73,8 @@ Json metrics_json(const SchedulerMetrics& m) {
   j["active_allocations"] = static_cast<int64_t>(m.active_allocations);
   j["allocated_gpus"] = static_cast<int64_t>(m.allocated_gpus);
   j["allocated_partitions"] = static_cast<int64_t>(m.allocated_partitions);
+  j["shared_gpus"] = static_cast<int64_t>(m.shared_gpus);
+  j["share_clients"] = static_cast<int64_t>(m.share_clients);
   return j;
 }
 
@@ -251,18 +259,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("release", [](PyPlatform& s, const std::string& uid, double now) { return s.p->release(uid, now); })
       .def("permit", [](PyPlatform& s, const std::string& uid) { return s.p->scheduler()->permit(uid); })
       .def("restore_allocation", [](PyPlatform& s, const std::string& js) {
-        Json j = Json::parse(js);
-        Allocation a;
-        a.uid = j.get("uid").str();
-        a.node = j.get("node").str();
-        a.ns = j.get("namespace").str("default");
-        a.team = j.get("team").str();
-        for (const auto& g : j.get("gpus").items()) a.gpus.push_back(g.str());
-        for (const auto& p : j.get("partitions").items()) a.partitions.push_back(p.str());
-        a.type = workload_type_from(j.get("type").str("Training"));
-        a.priority = j.get("priority").as_int(0);
-        a.preemptible = j.get("preemptible").as_bool(true);
-        return s.p->scheduler()->restore(a);
+        return s.p->scheduler()->restore(allocation_from_json(Json::parse(js)));
       })
       .def("allocations_json", [](PyPlatform& s) { return list_json(s.p->scheduler()->allocations()); })
       .def("scheduler_metrics_json", [](PyPlatform& s) { return metrics_json(s.p->scheduler()->metrics()).dump(); })
@@ -319,6 +316,18 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("reclaim_idle_partitions", [](PyPlatform& s, bool plan_only) {
         return list_json(s.p->partitions()->reclaim_idle(plan_only));
       }, py::arg("plan_only") = false)
+      .def("reclaim_idle_after", [](PyPlatform& s, double now, double min_idle_s) {
+        return list_json(s.p->partitions()->reclaim_idle_after(now, min_idle_s));
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("consolidate_partitions", [](PyPlatform& s, double now, bool plan_only) {
+        return s.p->consolidate_partitions(now, !plan_only);
+      }, py::arg("now"), py::arg("plan_only") = true, py::call_guard<py::gil_scoped_release>())
+      .def("pod_latency_quantile_ms", [](PyPlatform& s, double q) { return s.p->pod_latency().quantile_ms(q); })
+      .def("pod_latency_count", [](PyPlatform& s) { return s.p->pod_latency().count(); })
+      .def("queue_depth", [](PyPlatform& s) { return s.p->queue_depth(); })
+      .def("count_error", [](PyPlatform& s, const std::string& step) {
+        s.p->metrics()->add("kgwe_controller_errors_total", {step}, 1.0);
+      })
       .def("partition_ops_json", [](PyPlatform& s) { return list_json(s.p->partitions()->operations()); })
       .def("partition_metrics_json", [](PyPlatform& s) {
         PartitionMetrics pm = s.p->partitions()->metrics();
@@ -336,6 +345,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
         j["ops_total"] = pm.ops_total;
         j["ops_failed"] = pm.ops_failed;
         j["ops_pending"] = pm.ops_pending;
+        j["migrations"] = s.p->partitions()->migrations();
         return j.dump();
       })
       // ---- sharing
@@ -343,11 +353,14 @@ PYBIND11_MODULE(_kgwe_core, m) {
         Json j = Json::parse(js);
         SharingRequest r;
         r.uid = j.get("uid").str();
+        r.ns = j.get("namespace").str("default");
+        r.team = j.get("team").str();
+        r.method = sharing_method_from(j.get("method").str("None"));
         r.type = workload_type_from(j.get("type").str("Inference"));
         r.require_isolation = j.get("requireIsolation").as_bool(false);
         r.prefer_partition = j.get("preferPartition").as_bool(false);
         r.partition_mode = compute_partition_from(j.get("partitionMode").str("CPX"));
-        r.cu_percent = j.get("cuPercent").as_number(25.0);
+        r.cu_percent = j.get("cuPercent").as_number(0.0);
         r.memory_gb = j.get("memoryGB").as_number(0.0);
         r.node = j.get("node").str();
         r.gpu = j.get("gpu").str();
@@ -426,6 +439,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
         s.p->cost()->set_pricing(p);
       })
       .def("cost_replayed", [](PyPlatform& s) { return s.p->cost()->replayed(); })
+      .def("cost_resumed", [](PyPlatform& s) { return s.p->cost()->resumed(); })
       // ---- metrics / housekeeping
       .def("tick", [](PyPlatform& s, double now) { s.p->tick(now); }, py::call_guard<py::gil_scoped_release>())
       .def("expose_metrics", [](PyPlatform& s) { return s.p->expose_metrics(); },

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <ctime>
 #include <fstream>
 #include <sstream>
@@ -95,6 +96,8 @@ Json to_json(const UsageRecord& r) {
   j["peak_gfx"] = r.peak_gfx;
   j["idle_s"] = r.idle_s;
   j["sampled_s"] = r.sampled_s;
+  j["last_sample_s"] = r.last_sample_s;
+  j["peak_mem"] = r.peak_mem;
   j["raw_cost"] = r.raw_cost;
   j["adjusted_cost"] = r.adjusted_cost;
   j["finalized"] = r.finalized;
@@ -121,6 +124,8 @@ UsageRecord usage_from_json(const Json& j) {
   r.mem_integral = j.get("avg_mem").as_number(0) * r.sampled_s;
   r.peak_gfx = j.get("peak_gfx").as_number(0);
   r.idle_s = j.get("idle_s").as_number(0);
+  r.last_sample_s = j.get("last_sample_s").as_number(r.start_s + r.sampled_s);
+  r.peak_mem = j.get("peak_mem").as_number(0);
   r.raw_cost = j.get("raw_cost").as_number(0);
   r.adjusted_cost = j.get("adjusted_cost").as_number(0);
   r.finalized = j.get("finalized").as_bool(false);
@@ -243,7 +248,9 @@ std::string CostEngine::start(const UsageRecord& r0, double now_s) {
   if (r.gpu_type.empty()) r.gpu_type = "amd-mi355x-288gb";
   r.start_s = now_s;
   r.last_sample_s = now_s;
+  r.journaled_s = now_s;
   active_[r.uid] = r;
+  journal(r, "start");
   return "";
 }
 
@@ -260,6 +267,13 @@ bool CostEngine::sample(const std::string& uid, double gfx, double mem, double n
   r.peak_gfx = std::max(r.peak_gfx, gfx);
   r.peak_mem = std::max(r.peak_mem, mem);
   r.last_sample_s = now_s;
+  // Checkpoint the running record (integrals included) at most once per
+  // interval, so a controller restart / failover resumes it instead of
+  // losing the metered time.
+  if (now_s - r.journaled_s >= cfg_.journal_interval_s) {
+    r.journaled_s = now_s;
+    journal(r, "active");
+  }
   return true;
 }
 
@@ -388,7 +402,7 @@ bool CostEngine::finalize(const std::string& uid, double now_s, UsageRecord* out
       }
     }
     done_.push_back(r);
-    journal(r);
+    journal(r, "final");
   }
   if (hook_) hook_(r);
   if (out) *out = r;
@@ -670,27 +684,69 @@ double CostEngine::running_cost_per_hour() const {
   return c;
 }
 
-void CostEngine::journal(const UsageRecord& r) {
+// Caller holds mu_ (or runs single-threaded in the constructor).
+// Journal lines: {"ev": "start" | "active" | "final", "record": {...}}.
+void CostEngine::journal(const UsageRecord& r, const char* ev) {
   if (cfg_.journal_path.empty()) return;
   std::ofstream f(cfg_.journal_path, std::ios::app);
-  if (f) f << to_json(r).dump() << "\n";
+  if (!f) return;
+  Json j = Json::object();
+  j["ev"] = ev;
+  j["record"] = to_json(r);
+  f << j.dump() << "\n";
 }
 
 void CostEngine::replay() {
   if (cfg_.journal_path.empty()) return;
   std::ifstream f(cfg_.journal_path);
   std::string line;
+  std::map<std::string, UsageRecord> open;  // latest start / checkpoint per uid
   while (std::getline(f, line)) {
     if (line.empty()) continue;
     try {
-      UsageRecord r = usage_from_json(Json::parse(line));
-      r.finalized = true;
-      done_.push_back(r);
-      ++replayed_;
+      Json j = Json::parse(line);
+      const std::string ev = j.has("ev") ? j.get("ev").str() : "final";  // round-1 lines: finals
+      UsageRecord r = usage_from_json(j.has("record") ? j.get("record") : j);
+      if (ev == "final") {
+        r.finalized = true;
+        open.erase(r.uid);
+        done_.push_back(r);
+        ++replayed_;
+      } else {
+        r.finalized = false;
+        open[r.uid] = r;
+      }
     } catch (...) {
       // A torn final line (crash mid-write) is skipped, not fatal.
     }
   }
+  // Resume running records: the time between their last checkpoint and the
+  // next sample is metered at their last known utilisation by sample() /
+  // finalize(), so a failover loses no metered time.
+  for (auto& kv : open) {
+    kv.second.journaled_s = kv.second.last_sample_s;
+    active_[kv.first] = kv.second;
+    ++resumed_;
+  }
+  // Compact: finals + the open records' latest state, atomically.
+  const std::string tmp = cfg_.journal_path + ".compact";
+  {
+    std::ofstream o(tmp, std::ios::trunc);
+    if (!o) return;
+    for (const auto& r : done_) {
+      Json j = Json::object();
+      j["ev"] = "final";
+      j["record"] = to_json(r);
+      o << j.dump() << "\n";
+    }
+    for (const auto& kv : active_) {
+      Json j = Json::object();
+      j["ev"] = "active";
+      j["record"] = to_json(kv.second);
+      o << j.dump() << "\n";
+    }
+  }
+  std::rename(tmp.c_str(), cfg_.journal_path.c_str());
 }
 
 }  // namespace kgwe

@@ -12,9 +12,12 @@
 // > 5 records) and chargeback grouping.
 // Fixed / added: Project and Cluster budget scopes match; budget periods roll
 // over (Daily/Weekly/Monthly); enforcement is real (admit() => Block/Throttle);
-// utilisation is time-weighted from samples instead of overwritten; every
-// finalized record is journaled to an append-only JSONL file and replayed on
-// start (checkpoint/resume — the reference kept everything in memory);
+// utilisation is time-weighted from samples instead of overwritten; starts,
+// periodic checkpoints of RUNNING records and finals are journaled to an
+// append-only JSONL file, replayed and compacted on start — finished records
+// are restored and running ones resume metering (checkpoint/resume; the
+// reference designed TimescaleDB for this, values.yaml:283-294, and kept
+// everything in memory);
 // MI355X prices with compute-partition (CPX/QPX/DPX) fractional rates.
 #pragma once
 #include <functional>
@@ -58,6 +61,7 @@ struct UsageRecord {
   // Time-weighted utilisation integrals.
   double last_sample_s = 0, gfx_integral = 0, mem_integral = 0, idle_s = 0, sampled_s = 0;
   double peak_gfx = 0, peak_mem = 0;
+  double journaled_s = 0;  // last journal checkpoint (not serialized)
   double raw_cost = 0, adjusted_cost = 0;
   bool finalized = false;
 
@@ -109,6 +113,7 @@ struct CostEngineConfig {
   bool enable_rightsizing = true;
   double idle_threshold_pct = 5.0;  // gfx_activity below this counts as idle time
   std::string journal_path;         // "" = no persistence
+  double journal_interval_s = 60.0; // running-record checkpoint period
 };
 
 class CostEngine {
@@ -146,13 +151,14 @@ class CostEngine {
   // Metrics hook (wired to the Prometheus registry by the service layer).
   void set_cost_hook(std::function<void(const UsageRecord&)> f) { hook_ = std::move(f); }
   size_t replayed() const { return replayed_; }
+  size_t resumed() const { return resumed_; }  // running records restored from the journal
 
  private:
   bool in_scope(const UsageRecord& r, const std::string& scope, const std::string& id) const;
   bool applies(const Budget& b, const UsageRecord& r) const;
   void roll_period(Budget& b, double now_s) const;
   void check_alerts(Budget& b, double now_s);
-  void journal(const UsageRecord& r);
+  void journal(const UsageRecord& r, const char* ev);
   void replay();
 
   CostEngineConfig cfg_;
@@ -164,6 +170,7 @@ class CostEngine {
   std::vector<BudgetAlert> alerts_;
   int next_alert_ = 1;
   size_t replayed_ = 0;
+  size_t resumed_ = 0;
   std::function<void(const UsageRecord&)> hook_;
 };
 

@@ -214,6 +214,9 @@ void MetricRegistry::declare_kgwe_families() {
   declare("kgwe_partition_allocations_total", M::Counter, "Slice allocations", {"mode"});
   declare("kgwe_partition_releases_total", M::Counter, "Slice releases", {"mode"});
   declare("kgwe_partition_reconfigurations_total", M::Counter, "Partition mode switches", {"node", "result"});
+  declare("kgwe_partition_migrations_total", M::Counter, "Slices moved by partition consolidation", {});
+  declare("kgwe_gpu_share_clients", M::Gauge, "Co-located / time-sliced clients per GPU",
+          {"gpu_uuid", "node", "method"});
   // Interconnect
   declare("kgwe_xgmi_bandwidth_gbps", M::Gauge, "xGMI link bandwidth (measured, else rated)",
           {"gpu_uuid_1", "gpu_uuid_2", "node"});
@@ -228,7 +231,9 @@ void MetricRegistry::declare_kgwe_families() {
   // Workloads
   declare("kgwe_active_workloads", M::Gauge, "Active workloads", {"namespace", "workload_type"});
   declare("kgwe_workload_duration_seconds", M::Histogram, "Workload run time", {"workload_type"}, dur);
-  declare("kgwe_workload_queue_depth", M::Gauge, "Pending workloads", {});
+  declare("kgwe_workload_queue_depth", M::Gauge, "Pods filtered and not yet bound", {});
+  declare("kgwe_controller_errors_total", M::Counter, "Exceptions in the controller's periodic steps",
+          {"step"});
 }
 
 }  // namespace kgwe

@@ -70,6 +70,7 @@ class MetricRegistry {
 class GaugeBatch {
  public:
   void set(const std::string& name, MetricRegistry::Labels lv, double v) { fams_[name][std::move(lv)] = v; }
+  void add(const std::string& name, MetricRegistry::Labels lv, double v) { fams_[name][std::move(lv)] += v; }
   void touch(const std::string& name) { fams_[name]; }  // replace even when it ends up empty
 
  private:

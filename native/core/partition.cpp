@@ -143,22 +143,17 @@ bool PartitionController::gpu_idle(const GpuDevice& g) const {
 int PartitionController::free_slices(const ClusterTopology& c, ComputePartition mode,
                                      const MemoryPartition* memory) const {
   int n = 0;
+  std::set<std::string> owned;  // slices held in the ledger (one pass, not per slice)
+  if (sched_)
+    for (const auto& a : sched_->allocations())
+      for (const auto& p : a.partitions) owned.insert(p);
   for (const auto& kv : c.nodes)
     for (const auto& g : kv.second.gpus) {
       if (g.partition.compute != mode || !g.healthy() || g.partition.switching) continue;
       if (memory && g.partition.memory != *memory) continue;
       if (sched_ && g.partition.compute == ComputePartition::SPX && sched_->gpu_busy(g)) continue;
-      for (const auto& pi : g.partition.instances) {
-        if (pi.in_use) continue;
-        bool owned = false;
-        if (sched_) {
-          // A slice is owned when the ledger holds it; gpu_busy() is per GPU,
-          // so check slice ownership through the allocation list.
-          for (const auto& a : sched_->allocations())
-            if (std::find(a.partitions.begin(), a.partitions.end(), pi.id) != a.partitions.end()) owned = true;
-        }
-        n += owned ? 0 : 1;
-      }
+      for (const auto& pi : g.partition.instances)
+        n += (pi.in_use || owned.count(pi.id)) ? 0 : 1;
     }
   return n;
 }
@@ -369,6 +364,187 @@ std::vector<PartitionOp> PartitionController::reclaim_idle_after(double now_s, d
   return out;
 }
 
+Json to_json(const PartitionMove& m) {
+  Json j = Json::object();
+  j["uid"] = m.uid;
+  j["from"] = m.from;
+  j["to"] = m.to;
+  j["node_from"] = m.node_from;
+  j["node_to"] = m.node_to;
+  return j;
+}
+
+int PartitionController::migrations() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return migrations_;
+}
+
+std::vector<PartitionMove> PartitionController::consolidate(double now_s, const ConsolidationPolicy& pol,
+                                                            bool move_in_ledger) {
+  std::vector<PartitionMove> moves;
+  if (!sched_) return moves;
+  auto snap = disc_->snapshot();
+  // Donors emptied earlier (controller path: their pods were evicted) go
+  // back to SPX as soon as they are idle — no idle hysteresis for them.
+  std::set<std::string> draining;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    draining = draining_;
+  }
+  for (const auto& uuid : draining) {
+    for (const auto& kv : snap->nodes)
+      if (const GpuDevice* g = kv.second.gpu(uuid)) {
+        if (g->partition.compute == ComputePartition::SPX) {
+          std::lock_guard<std::mutex> lk(mu_);
+          draining_.erase(uuid);
+        } else if (gpu_idle(*g)) {
+          PartitionOp op = execute(kv.first, *g, ComputePartition::SPX, "consolidation: donor emptied", false);
+          if (op.state != OpState::Failed) {
+            std::lock_guard<std::mutex> lk(mu_);
+            draining_.erase(uuid);
+          }
+        }
+      }
+  }
+  snap = disc_->snapshot();
+  const auto allocs = sched_->allocations();
+  std::map<std::string, const Allocation*> owner;  // slice id -> allocation
+  for (const auto& a : allocs)
+    for (const auto& p : a.partitions) owner[p] = &a;
+  struct G {
+    std::string node;
+    const GpuDevice* g;
+    int used = 0, total = 0;
+    bool movable = true;
+    std::vector<std::string> free_slices, used_slices;
+  };
+  std::map<ComputePartition, std::vector<G>> by_mode;
+  std::map<std::string, double> low;
+  std::map<std::string, double> migrated;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    low = low_since_;
+    migrated = migrated_at_;
+    draining = draining_;
+  }
+  std::map<std::string, double> low_next;
+  for (const auto& kv : snap->nodes)
+    for (const auto& g : kv.second.gpus) {
+      if (g.partition.compute == ComputePartition::SPX || !g.healthy() || g.partition.switching) continue;
+      if (draining.count(g.uuid)) continue;
+      G e{kv.first, &g};
+      for (const auto& pi : g.partition.instances) {
+        e.total++;
+        auto o = owner.find(pi.id);
+        if (pi.in_use || o != owner.end()) {
+          e.used++;
+          e.used_slices.push_back(pi.id);
+          // Only preemptible inference / batch work that has not moved
+          // recently, holding nothing but slices, may be migrated.
+          const Allocation* a = o == owner.end() ? nullptr : o->second;
+          const bool ok = a && a->preemptible && a->gpus.empty() && a->gang.empty() &&
+                          (a->type == WorkloadType::Inference || a->type == WorkloadType::Batch) &&
+                          (!migrated.count(a->uid) || now_s - migrated[a->uid] >= pol.cooldown_s);
+          e.movable &= ok;
+        } else {
+          e.free_slices.push_back(pi.id);
+        }
+      }
+      if (e.total == 0) continue;
+      if (e.used > 0 && e.used < pol.below * e.total) {
+        auto it = low.find(g.uuid);
+        low_next[g.uuid] = it == low.end() ? now_s : it->second;
+      }
+      by_mode[g.partition.compute].push_back(std::move(e));
+    }
+  std::vector<std::string> emptied;
+  for (auto& mk : by_mode) {
+    auto& gs = mk.second;
+    // Donors: emptiest first.  Receivers: fullest first.
+    std::vector<G*> donors, recv;
+    for (auto& e : gs) {
+      auto l = low_next.find(e.g->uuid);
+      if (e.movable && l != low_next.end() && now_s - l->second >= pol.after_s) donors.push_back(&e);
+    }
+    std::sort(donors.begin(), donors.end(), [](const G* a, const G* b) {
+      return a->used != b->used ? a->used < b->used : a->g->uuid < b->g->uuid;
+    });
+    std::set<const G*> is_donor, gone;
+    for (auto* d : donors) is_donor.insert(d);
+    for (auto* d : donors) {
+      if (!is_donor.count(d)) continue;  // received slices meanwhile: no longer a donor
+      recv.clear();
+      for (auto& e : gs)
+        if (&e != d && !gone.count(&e) && !e.free_slices.empty()) recv.push_back(&e);
+      std::sort(recv.begin(), recv.end(), [&](const G* a, const G* b) {
+        const bool ad = is_donor.count(a) && !gone.count(a), bd = is_donor.count(b) && !gone.count(b);
+        if (ad != bd) return !ad;  // prefer non-donors
+        return a->used != b->used ? a->used > b->used : a->g->uuid < b->g->uuid;
+      });
+      // Later (fuller or equal) donors may receive: they stop being donors.
+      int room = 0;
+      for (auto* r : recv) room += static_cast<int>(r->free_slices.size());
+      if (room < d->used) continue;  // cannot be emptied completely: leave it
+      std::vector<PartitionMove> mine;
+      bool ok = true;
+      for (const auto& sl : d->used_slices) {
+        G* tgt = nullptr;
+        for (auto* r : recv)
+          if (!r->free_slices.empty()) {
+            tgt = r;
+            break;
+          }
+        if (!tgt) {
+          ok = false;
+          break;
+        }
+        PartitionMove m;
+        m.uid = owner.at(sl)->uid;
+        m.from = sl;
+        m.to = tgt->free_slices.back();
+        m.node_from = d->node;
+        m.node_to = tgt->node;
+        if (move_in_ledger && !sched_->migrate_partition(m.uid, m.from, m.to)) {
+          ok = false;
+          break;
+        }
+        tgt->free_slices.pop_back();
+        tgt->used++;
+        is_donor.erase(tgt);
+        mine.push_back(m);
+      }
+      if (!ok) continue;  // ledger moved underneath us: the rest waits for the next tick
+      gone.insert(d);
+      emptied.push_back(d->g->uuid);
+      for (auto& m : mine) moves.push_back(m);
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    low_since_.swap(low_next);
+    for (const auto& m : moves) migrated_at_[m.uid] = now_s;
+    migrations_ += static_cast<int>(moves.size());
+    for (const auto& u : emptied) {
+      draining_.insert(u);
+      low_since_.erase(u);
+    }
+    if (migrated_at_.size() > 100000) migrated_at_.clear();
+  }
+  if (move_in_ledger) {  // donors are empty right now: switch them back
+    auto s2 = disc_->snapshot();
+    for (const auto& u : emptied)
+      for (const auto& kv : s2->nodes)
+        if (const GpuDevice* g = kv.second.gpu(u)) {
+          PartitionOp op = execute(kv.first, *g, ComputePartition::SPX, "consolidation: donor emptied", false);
+          if (op.state != OpState::Failed) {
+            std::lock_guard<std::mutex> lk(mu_);
+            draining_.erase(u);
+          }
+        }
+  }
+  return moves;
+}
+
 std::vector<PartitionOp> PartitionController::operations() const {
   std::lock_guard<std::mutex> lk(mu_);
   return ops_;
@@ -411,23 +587,6 @@ PartitionMetrics PartitionController::metrics() const {
 // ---------------------------------------------------------------------------
 // sharing
 // ---------------------------------------------------------------------------
-const char* to_string(SharingMethod m) {
-  switch (m) {
-    case SharingMethod::None: return "None";
-    case SharingMethod::Partition: return "Partition";
-    case SharingMethod::CoLocate: return "CoLocate";
-    case SharingMethod::TimeSlice: return "TimeSlice";
-  }
-  return "None";
-}
-
-SharingMethod sharing_method_from(const std::string& s) {
-  if (s == "Partition" || s == "MIG") return SharingMethod::Partition;
-  if (s == "CoLocate" || s == "MPS") return SharingMethod::CoLocate;
-  if (s == "TimeSlice") return SharingMethod::TimeSlice;
-  return SharingMethod::None;
-}
-
 Json to_json(const SharingAllocation& a) {
   Json j = Json::object();
   j["uid"] = a.uid;
@@ -437,16 +596,39 @@ Json to_json(const SharingAllocation& a) {
   j["cu_begin"] = a.cu_begin;
   j["cu_end"] = a.cu_end;
   j["memory_gb"] = a.memory_gb;
+  j["gpu_index"] = a.gpu_index;
   Json env = Json::object();
   for (const auto& kv : a.env) env[kv.first] = kv.second;
   j["env"] = env;
   return j;
 }
 
-SharingManager::SharingManager(std::shared_ptr<DiscoveryService> disc, SharingPolicy policy)
-    : disc_(std::move(disc)), policy_(std::move(policy)) {}
+std::map<std::string, std::string> share_env(SharingMethod m, int gpu_index, int cu_begin, int cu_end,
+                                             double memory_gb, double gpu_memory_gb) {
+  std::map<std::string, std::string> env;
+  env["KGWE_SHARING"] = to_string(m);
+  env["HIP_VISIBLE_DEVICES"] = std::to_string(gpu_index);
+  env["ROCR_VISIBLE_DEVICES"] = std::to_string(gpu_index);
+  if (m == SharingMethod::CoLocate) {
+    // ROCm CU masking: <device index>:<CU list>; the device is 0 once
+    // ROCR_VISIBLE_DEVICES leaves only this GPU visible.
+    env["HSA_CU_MASK"] = "0:" + std::to_string(cu_begin) + "-" + std::to_string(cu_end - 1);
+    env["KGWE_CU_RANGE"] = std::to_string(cu_begin) + "-" + std::to_string(cu_end);
+  }
+  if (memory_gb > 0 && gpu_memory_gb > 0) {
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "%.4f", std::min(1.0, memory_gb / gpu_memory_gb));
+    env["KGWE_GPU_MEMORY_FRACTION"] = buf;
+  }
+  return env;
+}
+
+SharingManager::SharingManager(std::shared_ptr<DiscoveryService> disc, std::shared_ptr<Scheduler> sched,
+                               SharingPolicy policy)
+    : disc_(std::move(disc)), sched_(std::move(sched)), policy_(std::move(policy)) {}
 
 SharingMethod SharingManager::decide(const SharingRequest& r) const {
+  if (r.method != SharingMethod::None) return r.method;
   auto it = policy_.by_type.find(r.type);
   if (it != policy_.by_type.end()) return it->second;
   if (r.require_isolation) return SharingMethod::Partition;
@@ -454,11 +636,25 @@ SharingMethod SharingManager::decide(const SharingRequest& r) const {
   return SharingMethod::CoLocate;
 }
 
-int SharingManager::clients_on(const std::string& gpu) const {
-  std::lock_guard<std::mutex> lk(mu_);
-  int n = 0;
-  for (const auto& kv : allocs_) n += kv.second.gpu == gpu;
-  return n;
+int SharingManager::clients_on(const std::string& gpu) const { return sched_->share_clients(gpu); }
+
+SharingAllocation SharingManager::from_alloc(const Allocation& a) const {
+  SharingAllocation s;
+  s.uid = a.uid;
+  s.node = a.node;
+  s.gpu = a.shared_gpu;
+  s.method = a.sharing;
+  s.cu_begin = a.cu_begin;
+  s.cu_end = a.cu_end;
+  s.memory_gb = a.share_memory_gb;
+  GpuDevice g;
+  double mem = 0.0;
+  if (disc_->gpu(a.shared_gpu, &g)) {
+    s.gpu_index = g.index;
+    mem = g.memory_total_gb;
+  }
+  s.env = share_env(a.sharing, s.gpu_index, a.cu_begin, a.cu_end, a.share_memory_gb, mem);
+  return s;
 }
 
 SharingAllocation SharingManager::allocate(const SharingRequest& r, std::string* error) {
@@ -472,88 +668,38 @@ SharingAllocation SharingManager::allocate(const SharingRequest& r, std::string*
     a.env["KGWE_PARTITION_MODE"] = to_string(r.partition_mode);
     return a;
   }
-  GpuDevice g;
-  if (!disc_->gpu(r.gpu, &g)) {
-    *error = "unknown gpu " + r.gpu;
+  WorkloadRequest w;
+  w.uid = r.uid;
+  w.ns = r.ns;
+  w.team = r.team;
+  w.type = r.type;
+  w.sharing = a.method;
+  w.share_cu_percent = r.cu_percent;
+  w.share_memory_gb = r.memory_gb;
+  w.gpu_count = 1;
+  Decision d = sched_->reserve_share(w, r.node, r.gpu);
+  if (!d.ok) {
+    *error = d.failed_nodes.empty() ? "share rejected" : d.failed_nodes.begin()->second;
     return a;
   }
-  a.gpu_index = g.index;
-  std::lock_guard<std::mutex> lk(mu_);
-  if (allocs_.count(r.uid)) {
-    *error = "already allocated: " + r.uid;
+  Allocation al;
+  if (!sched_->allocation(r.uid, &al)) {
+    *error = "share vanished";
     return a;
   }
-  int clients = 0;
-  std::vector<std::pair<int, int>> used;
-  for (const auto& kv : allocs_)
-    if (kv.second.gpu == r.gpu) {
-      ++clients;
-      if (kv.second.method == SharingMethod::CoLocate) used.emplace_back(kv.second.cu_begin, kv.second.cu_end);
-    }
-  if (a.method == SharingMethod::TimeSlice) {
-    if (clients >= policy_.max_timeslice_replicas) {
-      *error = "time-slice replicas exhausted on " + r.gpu;
-      return a;
-    }
-    a.env["KGWE_SHARING"] = "TimeSlice";
-  } else {
-    if (clients >= policy_.max_clients_per_gpu) {
-      *error = "co-location client limit reached on " + r.gpu;
-      return a;
-    }
-    const double pct = r.cu_percent > 0 ? r.cu_percent : policy_.default_cu_percent;
-    int want = std::max(1, static_cast<int>(std::lround(g.cu_count * pct / 100.0)));
-    // Round to whole XCDs when possible (32 CUs share one L2).
-    const int per_xcd = g.xcd_count > 0 ? g.cu_count / g.xcd_count : g.cu_count;
-    if (want >= per_xcd) want = (want + per_xcd - 1) / per_xcd * per_xcd;
-    std::sort(used.begin(), used.end());
-    int start = 0, found = -1;
-    for (const auto& u : used) {
-      if (u.first - start >= want) {
-        found = start;
-        break;
-      }
-      start = std::max(start, u.second);
-    }
-    if (found < 0 && g.cu_count - start >= want) found = start;
-    if (found < 0) {
-      *error = "not enough free compute units on " + r.gpu;
-      return a;
-    }
-    double mem_used = 0.0;
-    for (const auto& kv : allocs_)
-      if (kv.second.gpu == r.gpu) mem_used += kv.second.memory_gb;
-    if (r.memory_gb > 0 && mem_used + r.memory_gb > g.memory_free_gb() + 1e-9) {
-      *error = "memory cap exceeds free HBM on " + r.gpu;
-      return a;
-    }
-    a.cu_begin = found;
-    a.cu_end = found + want;
-    a.memory_gb = r.memory_gb;
-    a.env["KGWE_SHARING"] = "CoLocate";
-    // ROCm CU masking: device-local index : CU list (HSA_CU_MASK syntax).
-    a.env["HSA_CU_MASK"] = "0:" + std::to_string(a.cu_begin) + "-" + std::to_string(a.cu_end - 1);
-    if (r.memory_gb > 0) {
-      char buf[32];
-      std::snprintf(buf, sizeof buf, "%.3f", r.memory_gb / g.memory_total_gb);
-      a.env["KGWE_GPU_MEMORY_FRACTION"] = buf;
-    }
-  }
-  a.env["HIP_VISIBLE_DEVICES"] = std::to_string(g.index);
-  a.env["ROCR_VISIBLE_DEVICES"] = std::to_string(g.index);
-  allocs_[r.uid] = a;
-  return a;
+  return from_alloc(al);
 }
 
 bool SharingManager::release(const std::string& uid) {
-  std::lock_guard<std::mutex> lk(mu_);
-  return allocs_.erase(uid) > 0;
+  Allocation a;
+  if (!sched_->allocation(uid, &a) || a.sharing == SharingMethod::None) return false;
+  return sched_->release(uid);
 }
 
 std::vector<SharingAllocation> SharingManager::allocations() const {
-  std::lock_guard<std::mutex> lk(mu_);
   std::vector<SharingAllocation> out;
-  for (const auto& kv : allocs_) out.push_back(kv.second);
+  for (const auto& a : sched_->allocations())
+    if (a.sharing != SharingMethod::None) out.push_back(from_alloc(a));
   return out;
 }
 

@@ -24,6 +24,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -65,6 +66,21 @@ struct PartitionOp {
 };
 Json to_json(const PartitionOp& op);
 
+// One slice moved by consolidation: `uid` leaves `from` for `to`.
+struct PartitionMove {
+  std::string uid, from, to, node_from, node_to;
+};
+Json to_json(const PartitionMove& m);
+
+// Consolidating rebalance (reference MIGController.Rebalance, a no-op there:
+// src/sharing/mig_controller.go:480-512; minUtilizationThreshold, CRD
+// gpuworkload-crd.yaml:248-366).
+struct ConsolidationPolicy {
+  double below = 0.75;         // a partitioned GPU with slice occupancy < this is a donor
+  double after_s = 120.0;      // ... once it has stayed below for this long (hysteresis)
+  double cooldown_s = 3600.0;  // a workload is migrated at most once per cooldown
+};
+
 struct PartitionMetrics {
   struct Mode {
     int gpus = 0, slices = 0, slices_in_use = 0;
@@ -99,6 +115,17 @@ class PartitionController {
   // `min_idle_s`, so a burst of partition pods does not thrash modes.
   std::vector<PartitionOp> reclaim_idle_after(double now_s, double min_idle_s);
 
+  // Empty under-used partitioned GPUs: move their preemptible inference
+  // slices onto the fullest GPUs of the same mode (only when a donor can be
+  // emptied completely), then switch the emptied GPU back to SPX.
+  // move_in_ledger: true -> the ledger moves the slices itself (simulation /
+  // direct API); false -> only plan: the controller evicts the pods (the
+  // recreated pods are packed onto the fuller GPUs by best fit) and the
+  // emptied donors are reclaimed on the next call.
+  std::vector<PartitionMove> consolidate(double now_s, const ConsolidationPolicy& pol,
+                                         bool move_in_ledger);
+  int migrations() const;
+
   std::vector<PartitionOp> operations() const;
   PartitionMetrics metrics() const;
   void set_dry_run(bool d) { dry_run_ = d; }
@@ -115,6 +142,10 @@ class PartitionController {
   mutable std::mutex mu_;
   std::map<std::string, PartitionStrategy> strategies_;
   std::map<std::string, double> idle_since_;  // partitioned GPU uuid -> first idle tick
+  std::map<std::string, double> low_since_;   // partitioned GPU uuid -> first under-used tick
+  std::map<std::string, double> migrated_at_; // workload uid -> last migration
+  std::set<std::string> draining_;            // donors emptied by consolidation
+  int migrations_ = 0;
   std::vector<PartitionOp> ops_;
   int next_op_ = 1;
 };
@@ -123,19 +154,20 @@ class PartitionController {
 // GPU sharing (reference src/sharing/mig_controller.go:545-857: MPS controller
 // + GPUSharingManager).  ROCm has no MPS daemon; the MI355X-native equivalent
 // of MPS's active-thread percentage is CU masking: each co-located client gets
-// a DISJOINT range of compute units through HSA_CU_MASK, plus a memory cap.
+// a DISJOINT range of compute units through HSA_CU_MASK, plus an HBM cap.
+// The CU ranges live in the scheduler LEDGER (Scheduler::shared_), so a GPU
+// with co-located clients is never handed out whole or partitioned, and a
+// whole / partitioned GPU never takes a client — one lock, no second book.
+// SharingManager is the policy + explicit-placement facade over it.
 // ---------------------------------------------------------------------------
-enum class SharingMethod { None, Partition, CoLocate, TimeSlice };
-const char* to_string(SharingMethod m);
-SharingMethod sharing_method_from(const std::string& s);
-
 struct SharingRequest {
-  std::string uid;
+  std::string uid, ns = "default", team;
   WorkloadType type = WorkloadType::Inference;
   bool require_isolation = false;
   bool prefer_partition = false;
+  SharingMethod method = SharingMethod::None;  // None: decided by policy
   ComputePartition partition_mode = ComputePartition::CPX;
-  double cu_percent = 25.0;
+  double cu_percent = 0.0;   // 0: scheduler default (one XCD)
   double memory_gb = 0.0;
   std::string node, gpu;  // target GPU for co-location / time-slicing
 };
@@ -150,29 +182,35 @@ struct SharingAllocation {
 };
 Json to_json(const SharingAllocation& a);
 
+// Container environment of a share: device visibility, HSA_CU_MASK (device-
+// local index 0 after HIP/ROCR_VISIBLE_DEVICES), memory cap as a fraction of
+// the GPU's HBM (KGWE_GPU_MEMORY_FRACTION, applied by kgwe.launch /
+// kgwe.utils.sharing through torch.cuda.set_per_process_memory_fraction).
+std::map<std::string, std::string> share_env(SharingMethod m, int gpu_index, int cu_begin, int cu_end,
+                                             double memory_gb, double gpu_memory_gb);
+
 struct SharingPolicy {
   std::map<WorkloadType, SharingMethod> by_type;
-  int max_clients_per_gpu = 8;
-  double default_cu_percent = 25.0;
-  int max_timeslice_replicas = 4;
 };
 
 class SharingManager {
  public:
-  SharingManager(std::shared_ptr<DiscoveryService> disc, SharingPolicy policy = {});
+  SharingManager(std::shared_ptr<DiscoveryService> disc, std::shared_ptr<Scheduler> sched,
+                 SharingPolicy policy = {});
   SharingMethod decide(const SharingRequest& r) const;
   // Partition method returns method=Partition and leaves slice choice to the
-  // scheduler; CoLocate / TimeSlice allocate here.  error set on failure.
+  // scheduler; CoLocate / TimeSlice reserve a client slot on r.gpu in the
+  // scheduler ledger.  error set on failure.
   SharingAllocation allocate(const SharingRequest& r, std::string* error);
   bool release(const std::string& uid);
   std::vector<SharingAllocation> allocations() const;
   int clients_on(const std::string& gpu) const;
 
  private:
+  SharingAllocation from_alloc(const Allocation& a) const;
   std::shared_ptr<DiscoveryService> disc_;
+  std::shared_ptr<Scheduler> sched_;
   SharingPolicy policy_;
-  mutable std::mutex mu_;
-  std::map<std::string, SharingAllocation> allocs_;
 };
 
 }  // namespace kgwe

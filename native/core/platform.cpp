@@ -70,6 +70,23 @@ WorkloadRequest workload_from_pod(const Json& pod, const std::string& gpu_resour
     w.gang = ann.get("kgwe.amd.com/gang").str();
     w.gang_size = std::atoi(ann.get("kgwe.amd.com/gang-size").str("0").c_str());
     w.preemptible = ann.get("kgwe.amd.com/preemptible").str("true") != "false";
+    // Co-located / time-sliced share of a whole GPU: amd.com/gpu-shared (or
+    // the kgwe.amd.com/sharing annotation) + CU percentage and HBM cap.
+    int64_t shared = 0;
+    for (const auto& c : spec.get("containers").items()) {
+      const Json& lim = c.get("resources").get("limits");
+      const std::string r = gpu_resource + "-shared";
+      shared += quantity(lim.has(r) ? lim.get(r) : c.get("resources").get("requests").get(r));
+    }
+    const std::string sm = ann.get("kgwe.amd.com/sharing").str(shared > 0 ? "CoLocate" : "");
+    if (!sm.empty() && sharing_method_from(sm) != SharingMethod::None &&
+        sharing_method_from(sm) != SharingMethod::Partition) {
+      w.sharing = sharing_method_from(sm);
+      w.gpu_count = 1;
+      w.share_cu_percent = std::atof(ann.get("kgwe.amd.com/cu-percent").str("0").c_str());
+      w.share_memory_gb = std::atof(ann.get("kgwe.amd.com/memory-gb").str("0").c_str());
+      if (!ann.has("kgwe.amd.com/workload-type")) w.type = WorkloadType::Inference;
+    }
   }
   if (spec.has("priority")) w.priority = spec.get("priority").as_int(w.priority);
   for (const auto& kv : spec.get("nodeSelector").fields()) w.node_selector[kv.first] = kv.second.str();
@@ -171,7 +188,7 @@ Platform::Platform(PlatformConfig cfg) : cfg_(std::move(cfg)) {
   sched_ = std::make_shared<Scheduler>(disc_, cfg_.sched);
   part_ = std::make_shared<PartitionController>(disc_, sched_, cfg_.partition_dry_run);
   SharingPolicy sp;
-  share_ = std::make_shared<SharingManager>(disc_, sp);
+  share_ = std::make_shared<SharingManager>(disc_, sched_, sp);
   cost_ = std::make_shared<CostEngine>(cfg_.cost);
   reg_ = std::make_shared<MetricRegistry>();
   reg_->declare_kgwe_families();
@@ -181,13 +198,20 @@ Platform::Platform(PlatformConfig cfg) : cfg_(std::move(cfg)) {
   });
 }
 
-void Platform::remember_pod(const std::string& uid, const WorkloadRequest& w) {
+void Platform::remember_pod(const std::string& uid, const WorkloadRequest& w, double created_s) {
   std::lock_guard<std::mutex> lk(pods_mu_);
   pods_[uid] = w;
   name_to_uid_[w.ns + "/" + w.name] = uid;
   if (pods_.size() > 100000) {  // bounded: drop arbitrary old entries
     pods_.erase(pods_.begin());
   }
+  // First sighting starts the pod's latency clock (a retried filter keeps it).
+  if (!pending_.count(uid)) pending_[uid] = {now_ns(), created_s};
+}
+
+size_t Platform::queue_depth() const {
+  std::lock_guard<std::mutex> lk(pods_mu_);
+  return pending_.size();
 }
 
 std::string Platform::filter(const std::string& body) {
@@ -201,7 +225,10 @@ std::string Platform::filter(const std::string& body) {
   }
   const Json& pod = field(args, "pod", "Pod");
   WorkloadRequest w = workload_from_pod(pod, cfg_.gpu_resource);
-  remember_pod(w.uid, w);
+  // Microsecond creation stamp written by kgwe's mutating webhook (the
+  // apiserver's creationTimestamp is whole seconds); else first filter call.
+  remember_pod(w.uid, w,
+               std::atof(pod.get("metadata").get("annotations").get("kgwe.amd.com/created-at").str("0").c_str()));
   std::vector<std::string> names;
   const Json& nodes = field(args, "nodes", "Nodes");
   const bool full_nodes = nodes.is_object();
@@ -285,6 +312,13 @@ std::string Platform::placement_json(const WorkloadRequest& w, const Decision& d
   if (d.ok && disc_->node(d.node, &n)) {
     for (const auto& kv : rccl_env(w, d, n, cfg_.master_port)) env[kv.first] = kv.second;
   }
+  if (d.ok && d.sharing != SharingMethod::None && !d.shared_gpu.empty()) {
+    GpuDevice g;
+    if (disc_->gpu(d.shared_gpu, &g))
+      for (const auto& kv : share_env(d.sharing, g.index, d.cu_begin, d.cu_end, d.share_memory_gb,
+                                      g.memory_total_gb))
+        env[kv.first] = kv.second;
+  }
   pl["env"] = env;
   pl["workload"] = to_json(w);
   return pl.dump();
@@ -342,6 +376,28 @@ std::string Platform::bind(const std::string& body, const std::string& pod_json)
     res["error"] = "gang " + w.gang + " waiting for members";
   } else {
     reg_->add("kgwe_scheduling_successes_total", {}, 1);
+    // Pod create -> bind latency, recorded by the extender itself at every
+    // successful bind (the reference declares the histogram and never feeds
+    // it: prometheus_exporter.go:643-648).
+    std::pair<int64_t, double> seen{0, 0.0};
+    {
+      std::lock_guard<std::mutex> lk(pods_mu_);
+      auto it = pending_.find(w.uid);
+      if (it != pending_.end()) {
+        seen = it->second;
+        pending_.erase(it);
+      }
+    }
+    double created = seen.second;
+    if (created <= 0 && !pod_json.empty()) {
+      try {
+        created = std::atof(Json::parse(pod_json).get("metadata").get("annotations")
+                                .get("kgwe.amd.com/created-at").str("0").c_str());
+      } catch (...) {
+      }
+    }
+    if (created > 0) observe_pod_latency_ms(std::max(0.0, (wall_s() - created) * 1000.0));
+    else if (seen.first > 0) observe_pod_latency_ms(static_cast<double>(now_ns() - seen.first) / 1e6);
     UsageRecord r;
     r.uid = w.uid;
     r.ns = w.ns;
@@ -372,6 +428,12 @@ std::string Platform::schedule(const std::string& workload_json) {
   if (d.ok) reg_->add("kgwe_scheduling_successes_total", {}, 1);
   else reg_->add("kgwe_scheduling_failures_total", {"unschedulable"}, 1);
   reg_->add("kgwe_preemptions_total", {}, static_cast<double>(d.preempted.size()));
+  // Victims lose their GPUs now: stop metering them (their pods must be
+  // evicted by the caller — the controller's eviction path).
+  for (const auto& v : d.preempted) {
+    UsageRecord r;
+    cost_->finalize(v, wall_s(), &r);
+  }
   return placement_json(w, d);
 }
 
@@ -379,7 +441,10 @@ std::string Platform::release(const std::string& uid, double now_s) {
   Allocation a;
   const bool had = sched_->allocation(uid, &a);
   bool ok = sched_->release(uid);
-  share_->release(uid);
+  {
+    std::lock_guard<std::mutex> lk(pods_mu_);
+    pending_.erase(uid);
+  }
   UsageRecord r;
   Json out = Json::object();
   out["released"] = ok;
@@ -399,7 +464,17 @@ std::string Platform::release(const std::string& uid, double now_s) {
 
 void Platform::observe_pod_latency_ms(double ms) {
   reg_->observe("kgwe_scheduling_latency_ms", {}, ms);
-  sched_->record_latency_ms(ms);
+  pod_latency_.record_ms(ms);
+}
+
+std::string Platform::consolidate_partitions(double now_s, bool move_in_ledger) {
+  auto moves = part_->consolidate(now_s, cfg_.consolidate, move_in_ledger);
+  Json out = Json::array();
+  for (const auto& m : moves) {
+    out.push_back(to_json(m));
+    reg_->add("kgwe_partition_migrations_total", {}, 1);
+  }
+  return out.dump();
 }
 
 void Platform::tick(double now_s) {
@@ -442,7 +517,8 @@ void Platform::refresh_gauges(double now_s) {
                         "kgwe_partition_instance_utilization_percent", "kgwe_xgmi_bandwidth_gbps",
                         "kgwe_xgmi_link_status", "kgwe_pcie_bandwidth_gbps", "kgwe_topology_score",
                         "kgwe_active_workloads", "kgwe_budget_utilization_percent",
-                        "kgwe_cost_savings_recommended_dollars", "kgwe_gpu_cost_per_hour_dollars"})
+                        "kgwe_cost_savings_recommended_dollars", "kgwe_gpu_cost_per_hour_dollars",
+                        "kgwe_gpu_share_clients"})
     batch.touch(f);
   std::set<std::string> owned_parts;
   for (const auto& a : sched_->allocations())
@@ -496,6 +572,9 @@ void Platform::refresh_gauges(double now_s) {
     double ts = 50.0 + (n.xgmi_fully_connected ? 30.0 : 0.0) + (links ? 20.0 * links_up / links : 0.0);
     batch.set("kgwe_topology_score", {n.name}, ts);
   }
+  for (const auto& a : sched_->allocations())
+    if (!a.shared_gpu.empty())
+      batch.add("kgwe_gpu_share_clients", {a.shared_gpu, a.node, to_string(a.sharing)}, 1.0);
   std::map<std::pair<std::string, std::string>, int> active;
   for (const auto& a : sched_->allocations()) active[{a.ns, to_string(a.type)}]++;
   for (const auto& kv : active)
@@ -507,8 +586,16 @@ void Platform::refresh_gauges(double now_s) {
   for (const auto& r : cost_->recommendations("", "")) saving[r.type] += r.saving;
   for (const auto& kv : saving) batch.set("kgwe_cost_savings_recommended_dollars", {kv.first}, kv.second);
   batch.set("kgwe_gpu_cost_per_hour_dollars", {"all"}, cost_->running_cost_per_hour());
+  {
+    // Pods filtered but never bound nor released within an hour were deleted
+    // behind our back (no release call): age them out of the queue.
+    std::lock_guard<std::mutex> lk(pods_mu_);
+    const int64_t horizon = now_ns() - static_cast<int64_t>(3600) * 1000000000;
+    for (auto it = pending_.begin(); it != pending_.end();)
+      it = it->second.first < horizon ? pending_.erase(it) : std::next(it);
+  }
   reg_->commit(std::move(batch));
-  reg_->set("kgwe_workload_queue_depth", {}, 0.0);
+  reg_->set("kgwe_workload_queue_depth", {}, static_cast<double>(queue_depth()));
 }
 
 std::string Platform::expose_metrics() {

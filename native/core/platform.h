@@ -38,6 +38,7 @@ struct PlatformConfig {
   bool enforce_budgets = true;
   int master_port = 29500;
   std::string gpu_resource = "amd.com/gpu";
+  ConsolidationPolicy consolidate;
 };
 
 // Pod (core/v1 JSON) -> workload request.  Sources, in order: annotation
@@ -72,6 +73,15 @@ class Platform {
   std::string schedule(const std::string& workload_json);
   std::string release(const std::string& uid, double now_s);
   void observe_pod_latency_ms(double ms);
+  // Pod create -> bind latency (the KPI; reference docs/PRD.md:440), fed by
+  // bind() itself from the pod's creation stamp or its first filter call.
+  const LatencyHistogram& pod_latency() const { return pod_latency_; }
+  // Pods seen by filter and not yet bound / released (kgwe_workload_queue_depth).
+  size_t queue_depth() const;
+  // Consolidating partition rebalance; JSON list of moves.  move_in_ledger:
+  // see PartitionController::consolidate.  The moved workloads' cost records
+  // keep running (same uid); pods must be restarted on their new slice.
+  std::string consolidate_partitions(double now_s, bool move_in_ledger);
 
   // Periodic sweep: gang timeouts, cost samples from telemetry, gauges.
   void tick(double now_s);
@@ -79,7 +89,7 @@ class Platform {
 
   // Remember the pod object for a uid between filter and bind (the bind
   // request only carries name/namespace/uid/node).
-  void remember_pod(const std::string& uid, const WorkloadRequest& w);
+  void remember_pod(const std::string& uid, const WorkloadRequest& w, double created_s = 0.0);
 
  private:
   std::string placement_json(const WorkloadRequest& w, const Decision& d);
@@ -92,9 +102,13 @@ class Platform {
   std::shared_ptr<SharingManager> share_;
   std::shared_ptr<CostEngine> cost_;
   std::shared_ptr<MetricRegistry> reg_;
-  std::mutex pods_mu_;
+  mutable std::mutex pods_mu_;
   std::map<std::string, WorkloadRequest> pods_;  // uid -> request (filter -> bind)
   std::map<std::string, std::string> name_to_uid_;
+  // uid -> (monotonic first-seen ns, wall-clock creation stamp or 0) for
+  // pods not yet bound: the latency origin and the queue.
+  std::map<std::string, std::pair<int64_t, double>> pending_;
+  LatencyHistogram pod_latency_;
 };
 
 }  // namespace kgwe

@@ -93,8 +93,24 @@ const char* to_string(SchedEventType t) {
     case SchedEventType::Preempted: return "Preempted";
     case SchedEventType::GangReady: return "GangReady";
     case SchedEventType::GangTimeout: return "GangTimeout";
+    case SchedEventType::Migrated: return "Migrated";
   }
   return "Unknown";
+}
+const char* to_string(SharingMethod m) {
+  switch (m) {
+    case SharingMethod::None: return "None";
+    case SharingMethod::Partition: return "Partition";
+    case SharingMethod::CoLocate: return "CoLocate";
+    case SharingMethod::TimeSlice: return "TimeSlice";
+  }
+  return "None";
+}
+SharingMethod sharing_method_from(const std::string& s) {
+  if (s == "Partition" || s == "MIG") return SharingMethod::Partition;
+  if (s == "CoLocate" || s == "MPS") return SharingMethod::CoLocate;
+  if (s == "TimeSlice") return SharingMethod::TimeSlice;
+  return SharingMethod::None;
 }
 
 // ---------------------------------------------------------------------------
@@ -153,6 +169,14 @@ WorkloadRequest workload_from_json(const Json& in) {
       w.partition_memory_set = true;
       w.partition_memory = memory_partition_from(part.get("memoryMode").str());
     }
+  }
+  const Json& share = req.get("sharing");
+  if (share.is_object()) {
+    w.sharing = sharing_method_from(share.get("method").str("CoLocate"));
+    if (w.sharing == SharingMethod::Partition) w.sharing = SharingMethod::None;  // use `partition`
+    w.share_cu_percent = share.get("cuPercent").as_number(0.0);
+    w.share_memory_gb = share.get("memoryGB").as_number(0.0);
+    if (w.sharing != SharingMethod::None) w.gpu_count = 1;
   }
   const Json& mig = req.get("mig");  // legacy MIG field: map profile size to a mode
   if (!w.partition && mig.is_object()) {
@@ -222,6 +246,11 @@ Json to_json(const WorkloadRequest& w) {
   j["preemptible"] = w.preemptible;
   j["gang"] = w.gang;
   j["gang_size"] = w.gang_size;
+  if (w.sharing != SharingMethod::None) {
+    j["sharing"] = to_string(w.sharing);
+    j["share_cu_percent"] = w.share_cu_percent;
+    j["share_memory_gb"] = w.share_memory_gb;
+  }
   return j;
 }
 
@@ -237,6 +266,13 @@ Json to_json(const Decision& d) {
   Json p = Json::array();
   for (const auto& x : d.partitions) p.push_back(x);
   j["partitions"] = p;
+  if (d.sharing != SharingMethod::None) {
+    j["sharing"] = to_string(d.sharing);
+    j["shared_gpu"] = d.shared_gpu;
+    j["cu_begin"] = d.cu_begin;
+    j["cu_end"] = d.cu_end;
+    j["share_memory_gb"] = d.share_memory_gb;
+  }
   j["score"] = d.score;
   j["bandwidth_gbps"] = d.bandwidth_gbps;
   j["latency_ms"] = d.latency_ms;
@@ -259,18 +295,50 @@ Json to_json(const Allocation& a) {
   j["namespace"] = a.ns;
   j["team"] = a.team;
   j["gang"] = a.gang;
+  j["gang_size"] = a.gang_size;
   Json g = Json::array();
   for (const auto& x : a.gpus) g.push_back(x);
   j["gpus"] = g;
   Json p = Json::array();
   for (const auto& x : a.partitions) p.push_back(x);
   j["partitions"] = p;
+  if (a.sharing != SharingMethod::None) {
+    j["sharing"] = to_string(a.sharing);
+    j["shared_gpu"] = a.shared_gpu;
+    j["cu_begin"] = a.cu_begin;
+    j["cu_end"] = a.cu_end;
+    j["share_memory_gb"] = a.share_memory_gb;
+  }
   j["type"] = to_string(a.type);
   j["priority"] = a.priority;
   j["preemptible"] = a.preemptible;
   j["gang_pending"] = a.gang_pending;
   j["bandwidth_gbps"] = a.bandwidth_gbps;
   return j;
+}
+
+// The inverse of to_json(Allocation): a ledger entry as the controller
+// persists it (pod annotations) and restores it after a restart / failover.
+Allocation allocation_from_json(const Json& j) {
+  Allocation a;
+  a.uid = j.get("uid").str();
+  a.node = j.get("node").str();
+  a.ns = j.get("namespace").str("default");
+  a.team = j.get("team").str();
+  a.gang = j.get("gang").str();
+  a.gang_size = static_cast<int>(j.get("gang_size").as_int(0));
+  for (const auto& g : j.get("gpus").items()) a.gpus.push_back(g.str());
+  for (const auto& p : j.get("partitions").items()) a.partitions.push_back(p.str());
+  a.sharing = sharing_method_from(j.get("sharing").str("None"));
+  a.shared_gpu = j.get("shared_gpu").str();
+  a.cu_begin = static_cast<int>(j.get("cu_begin").as_int(0));
+  a.cu_end = static_cast<int>(j.get("cu_end").as_int(0));
+  a.share_memory_gb = j.get("share_memory_gb").as_number(0.0);
+  a.type = workload_type_from(j.get("type").str("Training"));
+  a.priority = j.get("priority").as_int(0);
+  a.preemptible = j.get("preemptible").as_bool(true);
+  a.bandwidth_gbps = j.get("bandwidth_gbps").as_number(0.0);
+  return a;
 }
 
 // ---------------------------------------------------------------------------
@@ -370,7 +438,7 @@ std::vector<const GpuDevice*> Scheduler::free_gpus(const NodeTopology& n,
   for (const auto& g : n.gpus) {
     if (!g.healthy()) continue;
     if (g.partition.compute != ComputePartition::SPX || g.partition.switching) continue;
-    if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid)) continue;
+    if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid) || shared_.count(g.uuid)) continue;
     if (g.memory_free_gb() + 1e-9 < w.min_memory_gb) continue;
     if (!w.arch.empty() && g.arch != w.arch) continue;
     if (!w.model.empty() && g.model.find(w.model) == std::string::npos) continue;
@@ -387,7 +455,8 @@ std::vector<const PartitionInstance*> Scheduler::free_partitions(
     if (g.partition.compute != w.partition_mode) continue;
     if (w.partition_memory_set && g.partition.memory != w.partition_memory) continue;
     if (!w.arch.empty() && g.arch != w.arch) continue;
-    if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid)) continue;  // whole GPU taken / switching
+    if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid) || shared_.count(g.uuid))
+      continue;  // whole GPU taken / shared / switching
     for (const auto& pi : g.partition.instances) {
       if (pi.in_use || part_owner_.count(pi.id)) continue;
       if (pi.memory_gb + 1e-9 < w.min_memory_gb) continue;
@@ -436,6 +505,14 @@ std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w)
     auto it = allocs_.find(other);
     if (it != allocs_.end() && it->second.node != n.name)
       return "must co-locate with " + other + " on " + it->second.node;
+  }
+  if (w.sharing != SharingMethod::None) {
+    NodeScore tmp;
+    if (!pick_share(n, w, &tmp))
+      return std::string("no GPU can take a ") + to_string(w.sharing) + " client (" +
+             std::to_string(w.share_cu_percent > 0 ? w.share_cu_percent : cfg_.default_cu_percent) +
+             "% CUs, " + std::to_string(w.share_memory_gb) + " GB)";
+    return "";
   }
   if (w.partition) {
     auto parts = free_partitions(n, w, nullptr);
@@ -798,10 +875,103 @@ double Scheduler::bandwidth_of(const NodeTopology& n, const std::vector<std::str
   return pairs ? sum / pairs : 0.0;
 }
 
+// Caller holds mu_.  Can GPU g take the sharing client w?  CoLocate clients
+// get a disjoint CU range rounded to whole XCDs (32 CUs share one L2) when
+// the request is at least an XCD; TimeSlice clients share the whole GPU.
+bool Scheduler::share_fits(const GpuDevice& g, const WorkloadRequest& w, int* cu_begin, int* cu_end) const {
+  if (!g.healthy() || g.partition.compute != ComputePartition::SPX || g.partition.switching) return false;
+  if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid) || gpu_has_slice_owner_locked(g.uuid)) return false;
+  if (!w.arch.empty() && g.arch != w.arch) return false;
+  std::vector<const Allocation*> clients;
+  auto sh = shared_.find(g.uuid);
+  if (sh != shared_.end()) {
+    if (sh->second.method != w.sharing) return false;  // one method per GPU
+    for (const auto& uid : sh->second.clients) {
+      auto it = allocs_.find(uid);
+      if (it != allocs_.end()) clients.push_back(&it->second);
+    }
+  }
+  double mem = 0.0;
+  for (auto* c : clients) mem += c->share_memory_gb;
+  const double cap = g.memory_total_gb > 0 ? g.memory_total_gb : 288.0;
+  if (w.share_memory_gb > 0 && mem + w.share_memory_gb > cap + 1e-9) return false;
+  if (w.sharing == SharingMethod::TimeSlice) {
+    if (static_cast<int>(clients.size()) >= cfg_.max_timeslice_replicas) return false;
+    *cu_begin = 0;
+    *cu_end = g.cu_count > 0 ? g.cu_count : 256;
+    return true;
+  }
+  if (static_cast<int>(clients.size()) >= cfg_.max_share_clients) return false;
+  const int cus = g.cu_count > 0 ? g.cu_count : 256;
+  const int xcds = g.xcd_count > 0 ? g.xcd_count : 8;
+  const int per_xcd = cus / xcds;
+  const double pct = w.share_cu_percent > 0 ? w.share_cu_percent : cfg_.default_cu_percent;
+  int want = std::max(1, static_cast<int>(std::lround(cus * pct / 100.0)));
+  if (want >= per_xcd) want = (want + per_xcd - 1) / per_xcd * per_xcd;
+  if (want > cus) return false;
+  std::vector<std::pair<int, int>> used;
+  for (auto* c : clients) used.emplace_back(c->cu_begin, c->cu_end);
+  std::sort(used.begin(), used.end());
+  // Best fit among the free gaps (smallest gap that holds `want`), aligned to
+  // an XCD boundary when the request is XCD-sized.
+  const int align = want % per_xcd == 0 ? per_xcd : 1;
+  int best = -1, best_gap = 1 << 30, start = 0;
+  auto consider = [&](int lo, int hi) {
+    lo = (lo + align - 1) / align * align;
+    if (hi - lo >= want && hi - lo < best_gap) {
+      best = lo;
+      best_gap = hi - lo;
+    }
+  };
+  for (const auto& u : used) {
+    consider(start, u.first);
+    start = std::max(start, u.second);
+  }
+  consider(start, cus);
+  if (best < 0) return false;
+  *cu_begin = best;
+  *cu_end = best + want;
+  return true;
+}
+
+// Caller holds mu_.  Best fit: join the most loaded compatible shared GPU
+// (fewest CUs left after placement); open a fresh whole GPU only when none
+// has room — so whole GPUs stay free for training jobs.
+bool Scheduler::pick_share(const NodeTopology& n, const WorkloadRequest& w, NodeScore* s) const {
+  const GpuDevice* best = nullptr;
+  std::tuple<int, int, int> bkey{1, 0, 0};  // (fresh GPU?, -clients, index)
+  int bb = 0, be = 0;
+  for (const auto& g : n.gpus) {
+    int b = 0, e = 0;
+    if (!share_fits(g, w, &b, &e)) continue;
+    auto sh = shared_.find(g.uuid);
+    const int clients = sh == shared_.end() ? 0 : static_cast<int>(sh->second.clients.size());
+    std::tuple<int, int, int> key{clients == 0 ? 1 : 0, -clients, g.index};
+    if (!best || key < bkey) {
+      best = &g;
+      bkey = key;
+      bb = b;
+      be = e;
+    }
+  }
+  if (!best) return false;
+  s->shared_gpu = best->uuid;
+  s->cu_begin = bb;
+  s->cu_end = be;
+  return true;
+}
+
 NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w) const {
   NodeScore s;
   s.node = n.name;
-  if (w.partition) {
+  if (w.sharing != SharingMethod::None) {
+    if (!pick_share(n, w, &s)) return s;
+    auto sh = shared_.find(s.shared_gpu);
+    const int clients = sh == shared_.end() ? 0 : static_cast<int>(sh->second.clients.size());
+    s.topology = 100;
+    s.resource = clients > 0 ? 100 : 50;  // packing onto already-shared GPUs
+    s.balance = balance_score(n, clients > 0 ? 0 : 1);
+  } else if (w.partition) {
     std::vector<std::string> gpu_of;
     auto parts = free_partitions(n, w, &gpu_of);
     if (static_cast<int>(parts.size()) < w.partition_count) return s;
@@ -866,7 +1036,8 @@ bool Scheduler::gpu_has_slice_owner_locked(const std::string& gpu_uuid) const {
 
 bool Scheduler::fence_gpu(const std::string& gpu_uuid) {
   std::unique_lock<std::shared_mutex> lk(mu_);
-  if (gpu_owner_.count(gpu_uuid) || gpu_has_slice_owner_locked(gpu_uuid) || fenced_.count(gpu_uuid))
+  if (gpu_owner_.count(gpu_uuid) || gpu_has_slice_owner_locked(gpu_uuid) || fenced_.count(gpu_uuid) ||
+      shared_.count(gpu_uuid))
     return false;
   fenced_.insert(gpu_uuid);
   return true;
@@ -883,11 +1054,44 @@ void Scheduler::unfence_gpu(const std::string& gpu_uuid) {
 // while the GPU is fenced for a partition switch.
 bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending) {
   for (const auto& g : s.gpus)
-    if (gpu_owner_.count(g) || fenced_.count(g) || gpu_has_slice_owner_locked(g)) return false;
+    if (gpu_owner_.count(g) || fenced_.count(g) || gpu_has_slice_owner_locked(g) || shared_.count(g))
+      return false;
   for (const auto& p : s.partitions) {
     if (part_owner_.count(p)) return false;
     const std::string gpu = p.substr(0, p.rfind("/p"));
-    if (gpu_owner_.count(gpu) || fenced_.count(gpu)) return false;
+    if (gpu_owner_.count(gpu) || fenced_.count(gpu) || shared_.count(gpu)) return false;
+  }
+  if (w.sharing != SharingMethod::None) {
+    // Re-check the CU range against the ledger as it is now (the score may
+    // come from a concurrent reader's view).
+    if (s.shared_gpu.empty()) return false;
+    auto snap = disc_->snapshot();
+    auto nit = snap->nodes.find(s.node);
+    const GpuDevice* g = nit == snap->nodes.end() ? nullptr : nit->second.gpu(s.shared_gpu);
+    int b = 0, e = 0;
+    if (!g || !share_fits(*g, w, &b, &e)) return false;
+    if (b != s.cu_begin || e != s.cu_end) {
+      // the gap moved: take the range that fits now
+    }
+    Allocation a;
+    a.uid = w.uid;
+    a.node = s.node;
+    a.ns = w.ns;
+    a.team = w.team;
+    a.sharing = w.sharing;
+    a.shared_gpu = s.shared_gpu;
+    a.cu_begin = b;
+    a.cu_end = e;
+    a.share_memory_gb = w.share_memory_gb;
+    a.type = w.type;
+    a.priority = w.priority;
+    a.preemptible = w.preemptible;
+    a.allocated_ns = now_ns();
+    SharedGpu& sg = shared_[s.shared_gpu];
+    sg.method = w.sharing;
+    sg.clients.push_back(w.uid);
+    allocs_[w.uid] = std::move(a);
+    return true;
   }
   if (s.gpus.empty() && s.partitions.empty()) return false;
   Allocation a;
@@ -896,6 +1100,7 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
   a.ns = w.ns;
   a.team = w.team;
   a.gang = w.gang;
+  a.gang_size = w.gang_size;
   a.gpus = s.gpus;
   a.partitions = s.partitions;
   a.type = w.type;
@@ -909,6 +1114,23 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
   node_gpus_used_[s.node] += static_cast<int>(s.gpus.size());
   allocs_[w.uid] = std::move(a);
   return true;
+}
+
+// Caller holds mu_ exclusively: drop one ledger entry and everything it holds.
+void Scheduler::erase_locked(std::unordered_map<std::string, Allocation>::iterator it) {
+  const Allocation& a = it->second;
+  for (const auto& g : a.gpus) gpu_owner_.erase(g);
+  for (const auto& p : a.partitions) part_owner_.erase(p);
+  node_gpus_used_[a.node] -= static_cast<int>(a.gpus.size());
+  if (!a.shared_gpu.empty()) {
+    auto sh = shared_.find(a.shared_gpu);
+    if (sh != shared_.end()) {
+      auto& cl = sh->second.clients;
+      cl.erase(std::remove(cl.begin(), cl.end(), a.uid), cl.end());
+      if (cl.empty()) shared_.erase(sh);
+    }
+  }
+  allocs_.erase(it);
 }
 
 void Scheduler::emit(SchedEvent e) {
@@ -936,6 +1158,11 @@ static Decision decision_from(const Allocation& a, int score, const std::string&
   d.node = a.node;
   d.gpus = a.gpus;
   d.partitions = a.partitions;
+  d.sharing = a.sharing;
+  d.shared_gpu = a.shared_gpu;
+  d.cu_begin = a.cu_begin;
+  d.cu_end = a.cu_end;
+  d.share_memory_gb = a.share_memory_gb;
   d.score = score;
   d.bandwidth_gbps = a.bandwidth_gbps;
   return d;
@@ -951,14 +1178,8 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
     latency_.record_ms(dd.latency_ms);
     std::lock_guard<std::mutex> lk(stat_mu_);
     stats_.attempts++;
-    if (dd.ok) {
-      stats_.scheduled++;
-      if (dd.score > 0 && !dd.gpus.empty()) {
-        // topology-optimal = the chosen group's topology sub-score >= 80
-      }
-    } else {
-      stats_.failed++;
-    }
+    if (dd.ok) stats_.scheduled++;
+    else stats_.failed++;
   };
   {
     std::shared_lock<std::shared_mutex> lk(mu_);
@@ -980,7 +1201,8 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
           continue;
         }
         NodeScore s = score_node(kv.second, w);
-        if (s.total > 0 && (!s.gpus.empty() || !s.partitions.empty())) scores.push_back(std::move(s));
+        if (s.total > 0 && (!s.gpus.empty() || !s.partitions.empty() || !s.shared_gpu.empty()))
+          scores.push_back(std::move(s));
       }
     }
     std::sort(scores.begin(), scores.end(), [](const NodeScore& a, const NodeScore& b) {
@@ -992,21 +1214,23 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
       NodeScore s = scores[i];
       const NodeTopology& n = snap->nodes.at(s.node);
       bool stale = false;
-      for (const auto& g : s.gpus) stale |= gpu_owner_.count(g) > 0;
+      for (const auto& g : s.gpus) stale |= gpu_owner_.count(g) > 0 || shared_.count(g) > 0;
       for (const auto& p : s.partitions) stale |= part_owner_.count(p) > 0;
+      if (!s.shared_gpu.empty()) {
+        int b = 0, e = 0;
+        const GpuDevice* g = n.gpu(s.shared_gpu);
+        stale |= !g || !share_fits(*g, w, &b, &e);
+      }
       if (stale) {  // lost a race: re-score this node under the write lock
         if (!eligible(n, w).empty()) continue;
         s = score_node(n, w);
-        if (s.gpus.empty() && s.partitions.empty()) continue;
+        if (s.gpus.empty() && s.partitions.empty() && s.shared_gpu.empty()) continue;
       }
       const bool gang = cfg_.enable_gang && !w.gang.empty() && w.gang_size > 1;
       if (!reserve_locked(w, s, gang)) continue;
-      d.ok = true;
-      d.status = "Scheduled";
-      d.node = s.node;
-      d.gpus = s.gpus;
-      d.partitions = s.partitions;
-      d.score = s.total;
+      std::vector<std::string> preempted = std::move(d.preempted);
+      d = decision_from(allocs_.at(w.uid), s.total, "Scheduled");
+      d.preempted = std::move(preempted);
       d.bandwidth_gbps = s.bandwidth_gbps;
       d.reasons = s.reasons;
       d.failed_nodes.clear();
@@ -1054,6 +1278,20 @@ bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& sn
     std::vector<std::string> victims;
     std::tuple<int64_t, size_t, size_t> cost{INT64_MAX, 0, 0};
   } best;
+  // A gang is preempted as a unit: its other members (on any node) would
+  // otherwise keep their GPUs while the job cannot run.
+  auto unit_of = [&](const Allocation& a, std::vector<const Allocation*>* out) {
+    if (a.gang.empty()) {
+      out->push_back(&a);
+      return true;
+    }
+    for (const auto& kv : allocs_)
+      if (kv.second.gang == a.gang) {
+        if (!kv.second.preemptible || kv.second.priority >= w.priority) return false;
+        out->push_back(&kv.second);
+      }
+    return true;
+  };
   for (const auto& kv : snap->nodes) {
     std::vector<const Allocation*> cands;
     for (const auto& a : allocs_)
@@ -1064,23 +1302,41 @@ bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& sn
       if (a->priority != b->priority) return a->priority < b->priority;
       return a->allocated_ns > b->allocated_ns;  // youngest first: least work lost
     });
-    // Temporarily hide victims one by one until the node becomes eligible.
+    // Temporarily hide victims (whole gangs) one unit at a time until the node
+    // becomes eligible.
     std::vector<std::string> victims;
+    std::set<std::string> hidden_uids;
     std::vector<std::pair<std::string, std::string>> hidden_g, hidden_p;
+    std::vector<std::pair<std::string, SharedGpu>> hidden_s;
     int64_t prio = 0;
     size_t ngpu = 0;
     bool ok = false;
-    for (const Allocation* a : cands) {
-      victims.push_back(a->uid);
-      prio += a->priority;
-      ngpu += a->gpus.size() + a->partitions.size();
-      for (const auto& g : a->gpus) {
-        hidden_g.emplace_back(g, gpu_owner_[g]);
-        gpu_owner_.erase(g);
-      }
-      for (const auto& p : a->partitions) {
-        hidden_p.emplace_back(p, part_owner_[p]);
-        part_owner_.erase(p);
+    for (const Allocation* c : cands) {
+      if (hidden_uids.count(c->uid)) continue;
+      std::vector<const Allocation*> unit;
+      if (!unit_of(*c, &unit)) continue;
+      for (const Allocation* a : unit) {
+        if (!hidden_uids.insert(a->uid).second) continue;
+        victims.push_back(a->uid);
+        prio += a->priority;
+        ngpu += a->gpus.size() + a->partitions.size() + (a->shared_gpu.empty() ? 0 : 1);
+        for (const auto& g : a->gpus) {
+          hidden_g.emplace_back(g, gpu_owner_[g]);
+          gpu_owner_.erase(g);
+        }
+        for (const auto& p : a->partitions) {
+          hidden_p.emplace_back(p, part_owner_[p]);
+          part_owner_.erase(p);
+        }
+        if (!a->shared_gpu.empty()) {
+          auto sh = shared_.find(a->shared_gpu);
+          if (sh != shared_.end()) {
+            hidden_s.emplace_back(sh->first, sh->second);
+            auto& cl = sh->second.clients;
+            cl.erase(std::remove(cl.begin(), cl.end(), a->uid), cl.end());
+            if (cl.empty()) shared_.erase(sh);
+          }
+        }
       }
       if (eligible(kv.second, w).empty()) {
         ok = true;
@@ -1089,6 +1345,8 @@ bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& sn
     }
     for (auto& h : hidden_g) gpu_owner_[h.first] = h.second;
     for (auto& h : hidden_p) part_owner_[h.first] = h.second;
+    // Restore shares in reverse so the earliest (fullest) snapshot wins.
+    for (auto it = hidden_s.rbegin(); it != hidden_s.rend(); ++it) shared_[it->first] = it->second;
     if (!ok) continue;
     std::tuple<int64_t, size_t, size_t> cost{prio, victims.size(), ngpu};
     if (cost < best.cost) {
@@ -1101,13 +1359,18 @@ bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& sn
   for (const auto& uid : best.victims) {
     auto it = allocs_.find(uid);
     if (it == allocs_.end()) continue;
-    for (const auto& g : it->second.gpus) gpu_owner_.erase(g);
-    for (const auto& p : it->second.partitions) part_owner_.erase(p);
-    node_gpus_used_[it->second.node] -= static_cast<int>(it->second.gpus.size());
-    if (!it->second.gang.empty()) gangs_[it->second.gang].members.erase(uid);
-    allocs_.erase(it);
+    const std::string gang = it->second.gang;
+    const std::string node = it->second.node;
+    erase_locked(it);
+    if (!gang.empty()) {
+      auto g = gangs_.find(gang);
+      if (g != gangs_.end()) {
+        g->second.members.erase(uid);
+        if (g->second.members.empty()) gangs_.erase(g);
+      }
+    }
     d->preempted.push_back(uid);
-    emit({SchedEventType::Preempted, uid, best.node, "by " + w.uid, now_ns()});
+    emit({SchedEventType::Preempted, uid, node, "by " + w.uid, now_ns()});
   }
   std::lock_guard<std::mutex> sl(stat_mu_);
   stats_.preemptions += best.victims.size();
@@ -1121,53 +1384,120 @@ std::vector<Decision> Scheduler::schedule_gang(const std::vector<WorkloadRequest
   std::unique_lock<std::shared_mutex> lk(mu_);
   std::vector<std::string> placed;
   bool ok = true;
-  for (const auto& w : members) {
-    Decision d;
-    d.uid = w.uid;
-    NodeScore best;
-    for (const auto& kv : snap->nodes) {
-      std::string why = eligible(kv.second, w);
-      if (!why.empty()) {
-        d.failed_nodes[kv.first] = why;
-        continue;
-      }
-      NodeScore s = score_node(kv.second, w);
-      if ((s.gpus.empty() && s.partitions.empty()) || s.total <= 0) continue;
-      if (s.total > best.total || (s.total == best.total && s.node < best.node)) best = s;
-    }
-    WorkloadRequest wm = w;
-    wm.gang.clear();  // the whole gang is placed atomically here
-    if (best.node.empty() || !reserve_locked(wm, best, false)) {
-      ok = false;
-      d.status = "Unschedulable";
-      out.push_back(d);
-      break;
-    }
-    allocs_[w.uid].gang = w.gang;
-    placed.push_back(w.uid);
+  auto fill = [](Decision& d, const NodeScore& s) {
     d.ok = true;
     d.status = "Scheduled";
-    d.node = best.node;
-    d.gpus = best.gpus;
-    d.partitions = best.partitions;
-    d.score = best.total;
-    d.bandwidth_gbps = best.bandwidth_gbps;
-    d.reasons = best.reasons;
-    out.push_back(d);
+    d.node = s.node;
+    d.gpus = s.gpus;
+    d.partitions = s.partitions;
+    d.score = s.total;
+    d.bandwidth_gbps = s.bandwidth_gbps;
+    d.reasons = s.reasons;
+  };
+  // One xGMI island first: a gang of whole-GPU members that together fit one
+  // node and asked for xGMI connectivity (or runs a comm-heavy strategy) is
+  // placed as ONE group on one node — its ranks' collectives then ride the
+  // all-to-all xGMI mesh instead of the node NICs.  xGMIRequired gangs never
+  // spill across nodes.
+  int total = 0;
+  bool whole = true, want_island = false, need_island = false;
+  for (const auto& w : members) {
+    total += w.gpu_count;
+    whole &= !w.partition && w.sharing == SharingMethod::None && w.gpu_count > 0;
+    want_island |= w.topology == TopologyPreference::XgmiOptimal ||
+                   w.topology == TopologyPreference::XgmiRequired || comm_heavy(w.strategy) ||
+                   w.strategy == DistributionStrategy::DataParallel || w.strategy == DistributionStrategy::FSDP;
+    need_island |= w.topology == TopologyPreference::XgmiRequired;
+  }
+  if (whole && want_island && members.size() > 1) {
+    WorkloadRequest merged = members.front();
+    merged.gpu_count = total;
+    merged.gang.clear();
+    if (merged.topology == TopologyPreference::None) merged.topology = TopologyPreference::XgmiOptimal;
+    NodeScore best;
+    for (const auto& kv : snap->nodes) {
+      bool all = true;
+      for (const auto& w : members) all &= eligible(kv.second, w).empty();
+      if (!all || !eligible(kv.second, merged).empty()) continue;
+      NodeScore s = score_node(kv.second, merged);
+      if (static_cast<int>(s.gpus.size()) != total || s.total <= 0) continue;
+      if (s.total > best.total || (s.total == best.total && s.node < best.node)) best = s;
+    }
+    if (!best.node.empty()) {
+      size_t off = 0;
+      for (const auto& w : members) {
+        NodeScore part = best;
+        part.gpus.assign(best.gpus.begin() + off, best.gpus.begin() + off + w.gpu_count);
+        off += w.gpu_count;
+        WorkloadRequest wm = w;
+        wm.gang.clear();
+        Decision d;
+        d.uid = w.uid;
+        if (!reserve_locked(wm, part, false)) {
+          ok = false;
+          d.status = "Unschedulable";
+          out.push_back(d);
+          break;
+        }
+        allocs_[w.uid].gang = w.gang;
+        allocs_[w.uid].gang_size = w.gang_size;
+        placed.push_back(w.uid);
+        fill(d, part);
+        out.push_back(d);
+      }
+    } else if (need_island) {
+      ok = false;
+      for (const auto& w : members) {
+        Decision d;
+        d.uid = w.uid;
+        d.status = "Unschedulable";
+        d.reasons.push_back("no single node has " + std::to_string(total) + " free xGMI-connected GPUs");
+        out.push_back(d);
+      }
+    }
+  }
+  if (ok && out.empty()) {
+    for (const auto& w : members) {
+      Decision d;
+      d.uid = w.uid;
+      NodeScore best;
+      for (const auto& kv : snap->nodes) {
+        std::string why = eligible(kv.second, w);
+        if (!why.empty()) {
+          d.failed_nodes[kv.first] = why;
+          continue;
+        }
+        NodeScore s = score_node(kv.second, w);
+        if ((s.gpus.empty() && s.partitions.empty() && s.shared_gpu.empty()) || s.total <= 0) continue;
+        if (s.total > best.total || (s.total == best.total && s.node < best.node)) best = s;
+      }
+      WorkloadRequest wm = w;
+      wm.gang.clear();  // the whole gang is placed atomically here
+      if (best.node.empty() || !reserve_locked(wm, best, false)) {
+        ok = false;
+        d.status = "Unschedulable";
+        out.push_back(d);
+        break;
+      }
+      allocs_[w.uid].gang = w.gang;
+      allocs_[w.uid].gang_size = w.gang_size;
+      placed.push_back(w.uid);
+      d = decision_from(allocs_.at(w.uid), best.total, "Scheduled");
+      d.reasons = best.reasons;
+      out.push_back(d);
+    }
   }
   if (!ok) {  // roll back: all or nothing
     for (const auto& uid : placed) {
       auto it = allocs_.find(uid);
-      for (const auto& g : it->second.gpus) gpu_owner_.erase(g);
-      for (const auto& p : it->second.partitions) part_owner_.erase(p);
-      node_gpus_used_[it->second.node] -= static_cast<int>(it->second.gpus.size());
-      allocs_.erase(it);
+      if (it != allocs_.end()) erase_locked(it);
     }
     for (auto& d : out) {
       d.ok = false;
       d.status = "Unschedulable";
       d.gpus.clear();
       d.partitions.clear();
+      d.shared_gpu.clear();
     }
   }
   lk.unlock();
@@ -1256,12 +1586,7 @@ Decision Scheduler::bind(const WorkloadRequest& w, const std::string& node) {
     stats_.failed++;
     return d;
   }
-  d.ok = true;
-  d.status = "Scheduled";
-  d.node = node;
-  d.gpus = s.gpus;
-  d.partitions = s.partitions;
-  d.score = s.total;
+  d = decision_from(allocs_.at(w.uid), s.total, "Scheduled");
   d.bandwidth_gbps = s.bandwidth_gbps;
   d.reasons = s.reasons;
   if (gang) {
@@ -1281,6 +1606,7 @@ Decision Scheduler::bind(const WorkloadRequest& w, const std::string& node) {
   lk.unlock();
   emit({SchedEventType::Scheduled, w.uid, node, "", now_ns()});
   d.latency_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  latency_.record_ms(d.latency_ms);  // core bind latency (pod create -> bind is the Platform's)
   std::lock_guard<std::mutex> sl(stat_mu_);
   stats_.attempts++;
   stats_.scheduled++;
@@ -1310,11 +1636,7 @@ void Scheduler::expire_gangs() {
           now - g.first_ns > static_cast<int64_t>(cfg_.gang_timeout_ms) * 1000000) {
         for (const auto& uid : g.members) {
           auto a = allocs_.find(uid);
-          if (a == allocs_.end()) continue;
-          for (const auto& gp : a->second.gpus) gpu_owner_.erase(gp);
-          for (const auto& p : a->second.partitions) part_owner_.erase(p);
-          node_gpus_used_[a->second.node] -= static_cast<int>(a->second.gpus.size());
-          allocs_.erase(a);
+          if (a != allocs_.end()) erase_locked(a);
         }
         expired.push_back(it->first);
         it = gangs_.erase(it);
@@ -1337,9 +1659,6 @@ bool Scheduler::release(const std::string& uid) {
     auto it = allocs_.find(uid);
     if (it == allocs_.end()) return false;
     node = it->second.node;
-    for (const auto& g : it->second.gpus) gpu_owner_.erase(g);
-    for (const auto& p : it->second.partitions) part_owner_.erase(p);
-    node_gpus_used_[node] -= static_cast<int>(it->second.gpus.size());
     if (!it->second.gang.empty()) {
       auto g = gangs_.find(it->second.gang);
       if (g != gangs_.end()) {
@@ -1347,7 +1666,7 @@ bool Scheduler::release(const std::string& uid) {
         if (g->second.members.empty()) gangs_.erase(g);
       }
     }
-    allocs_.erase(it);
+    erase_locked(it);
   }
   emit({SchedEventType::Released, uid, node, "", now_ns()});
   std::lock_guard<std::mutex> sl(stat_mu_);
@@ -1359,21 +1678,106 @@ bool Scheduler::restore(const Allocation& a) {
   std::unique_lock<std::shared_mutex> lk(mu_);
   if (allocs_.count(a.uid)) return false;
   for (const auto& g : a.gpus)
-    if (gpu_owner_.count(g)) return false;
+    if (gpu_owner_.count(g) || shared_.count(g)) return false;
   for (const auto& p : a.partitions)
     if (part_owner_.count(p)) return false;
+  if (!a.shared_gpu.empty()) {
+    if (gpu_owner_.count(a.shared_gpu)) return false;
+    auto sh = shared_.find(a.shared_gpu);
+    if (sh != shared_.end() && sh->second.method != a.sharing) return false;
+  }
   for (const auto& g : a.gpus) gpu_owner_[g] = a.uid;
   for (const auto& p : a.partitions) part_owner_[p] = a.uid;
   node_gpus_used_[a.node] += static_cast<int>(a.gpus.size());
+  if (!a.shared_gpu.empty()) {
+    SharedGpu& sg = shared_[a.shared_gpu];
+    sg.method = a.sharing;
+    sg.clients.push_back(a.uid);
+  }
   Allocation c = a;
   if (!c.allocated_ns) c.allocated_ns = now_ns();
+  if (!c.gang.empty()) {  // a restored gang was complete when it was bound
+    Gang& gg = gangs_[c.gang];
+    gg.size = std::max(gg.size, c.gang_size);
+    gg.members.insert(c.uid);
+    gg.ready = true;
+    if (!gg.first_ns) gg.first_ns = c.allocated_ns;
+    c.gang_pending = false;
+  }
   allocs_[a.uid] = c;
   return true;
 }
 
+bool Scheduler::migrate_partition(const std::string& uid, const std::string& from, const std::string& to) {
+  std::string node;
+  {
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    auto it = allocs_.find(uid);
+    if (it == allocs_.end()) return false;
+    auto& parts = it->second.partitions;
+    auto pos = std::find(parts.begin(), parts.end(), from);
+    if (pos == parts.end() || part_owner_.count(to)) return false;
+    const std::string gpu = to.substr(0, to.rfind("/p"));
+    if (gpu_owner_.count(gpu) || fenced_.count(gpu) || shared_.count(gpu)) return false;
+    auto snap = disc_->snapshot();
+    std::string to_node;
+    for (const auto& kv : snap->nodes)
+      if (kv.second.gpu(gpu)) to_node = kv.first;
+    if (to_node.empty()) return false;
+    // A multi-slice allocation stays on one node.
+    if (parts.size() > 1 && to_node != it->second.node) return false;
+    part_owner_.erase(from);
+    part_owner_[to] = uid;
+    *pos = to;
+    it->second.node = to_node;
+    node = to_node;
+  }
+  emit({SchedEventType::Migrated, uid, node, from + " -> " + to, now_ns()});
+  return true;
+}
+
+Decision Scheduler::reserve_share(const WorkloadRequest& w, const std::string& node, const std::string& gpu) {
+  Decision d;
+  d.uid = w.uid;
+  d.status = "Unschedulable";
+  auto snap = disc_->snapshot();
+  auto nit = snap->nodes.find(node);
+  const GpuDevice* g = nit == snap->nodes.end() ? nullptr : nit->second.gpu(gpu);
+  if (!g || w.sharing == SharingMethod::None || w.sharing == SharingMethod::Partition) {
+    d.failed_nodes[node] = g ? "not a CoLocate / TimeSlice request" : "unknown gpu " + gpu;
+    return d;
+  }
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  if (allocs_.count(w.uid)) {
+    d.failed_nodes[node] = "already allocated: " + w.uid;
+    return d;
+  }
+  NodeScore s;
+  s.node = node;
+  if (!share_fits(*g, w, &s.cu_begin, &s.cu_end)) {
+    d.failed_nodes[node] = "no room for a " + std::string(to_string(w.sharing)) + " client on " + gpu;
+    return d;
+  }
+  s.shared_gpu = gpu;
+  if (!reserve_locked(w, s, false)) {
+    d.failed_nodes[node] = "reservation conflict";
+    return d;
+  }
+  d = decision_from(allocs_.at(w.uid), 100, "Scheduled");
+  lk.unlock();
+  emit({SchedEventType::Scheduled, w.uid, node, "share", now_ns()});
+  return d;
+}
+
+int Scheduler::share_clients(const std::string& gpu_uuid) const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  auto it = shared_.find(gpu_uuid);
+  return it == shared_.end() ? 0 : static_cast<int>(it->second.clients.size());
+}
+
 bool Scheduler::gpu_busy(const GpuDevice& g) const {
   std::shared_lock<std::shared_mutex> lk(mu_);
-  if (gpu_owner_.count(g.uuid)) return true;
+  if (gpu_owner_.count(g.uuid) || shared_.count(g.uuid)) return true;
   for (const auto& pi : g.partition.instances)
     if (part_owner_.count(pi.id)) return true;
   return false;
@@ -1411,6 +1815,8 @@ SchedulerMetrics Scheduler::metrics() const {
   m.active_allocations = allocs_.size();
   m.allocated_gpus = gpu_owner_.size();
   m.allocated_partitions = part_owner_.size();
+  m.shared_gpus = shared_.size();
+  for (const auto& kv : shared_) m.share_clients += kv.second.clients.size();
   return m;
 }
 

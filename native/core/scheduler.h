@@ -49,6 +49,12 @@ enum class DistributionStrategy { None, DataParallel, ModelParallel, PipelinePar
                                   FSDP, DeepSpeed, ContextParallel, ExpertParallel };
 enum class CommBackend { RCCL, Gloo, MPI };
 enum class ScoringMode { Xgmi, Compat };
+// GPU sharing without compute partitions (reference MPS / time-slicing,
+// src/sharing/mig_controller.go:545-857).  Partition = a CPX/QPX/DPX slice,
+// held through the partition fields of the request instead.
+enum class SharingMethod { None, Partition, CoLocate, TimeSlice };
+const char* to_string(SharingMethod m);
+SharingMethod sharing_method_from(const std::string& s);
 
 const char* to_string(TopologyPreference p);
 const char* to_string(WorkloadType t);
@@ -98,6 +104,11 @@ struct WorkloadRequest {
   std::vector<std::string> anti_affinity_with;
   std::string gang;
   int gang_size = 0;
+  // Co-located / time-sliced share of ONE whole SPX GPU (no partition
+  // switch): a disjoint CU range (HSA_CU_MASK) plus an HBM cap per client.
+  SharingMethod sharing = SharingMethod::None;
+  double share_cu_percent = 0.0;   // 0 = policy default
+  double share_memory_gb = 0.0;    // 0 = no cap
   double max_latency_ms = 0.0;
   std::vector<std::string> preferred_nodes;  // optimizer hint (+10 bonus)
 };
@@ -110,14 +121,22 @@ struct NodeScore {
   int total = 0, topology = 0, resource = 0, balance = 0, affinity = 0;
   std::vector<std::string> gpus;        // selected whole GPUs
   std::vector<std::string> partitions;  // selected partition slices
+  std::string shared_gpu;               // sharing requests: the GPU to join
+  int cu_begin = 0, cu_end = 0;
   double bandwidth_gbps = 0.0;
   std::vector<std::string> reasons;
 };
 
 struct Allocation {
   std::string uid, node, ns, team, gang;
+  int gang_size = 0;
   std::vector<std::string> gpus;
   std::vector<std::string> partitions;
+  // Sharing: the one GPU co-located / time-sliced with other clients.
+  SharingMethod sharing = SharingMethod::None;
+  std::string shared_gpu;
+  int cu_begin = 0, cu_end = 0;  // [begin, end) of the GPU's CUs (CoLocate)
+  double share_memory_gb = 0.0;
   WorkloadType type = WorkloadType::Training;
   int64_t priority = 0;
   bool preemptible = true;
@@ -131,6 +150,10 @@ struct Decision {
   std::string status;  // Scheduled | Waiting (gang) | Unschedulable
   std::string uid, node;
   std::vector<std::string> gpus, partitions;
+  std::string shared_gpu;
+  SharingMethod sharing = SharingMethod::None;
+  int cu_begin = 0, cu_end = 0;
+  double share_memory_gb = 0.0;
   int score = 0;
   double bandwidth_gbps = 0.0;
   double latency_ms = 0.0;
@@ -141,6 +164,7 @@ struct Decision {
 
 Json to_json(const Decision& d);
 Json to_json(const Allocation& a);
+Allocation allocation_from_json(const Json& j);
 
 struct SchedulerConfig {
   int topology_weight = 40, resource_weight = 35, balance_weight = 25;
@@ -154,9 +178,13 @@ struct SchedulerConfig {
   double degraded_link_ratio = 0.7;  // measured/rated below this => degraded link
   size_t event_capacity = 4096;
   size_t exhaustive_limit = 4096;  // max combinations enumerated per node
+  // Sharing policy (reference MPSControllerConfig, mig_controller.go:559-581).
+  int max_share_clients = 8;          // co-located clients per GPU
+  double default_cu_percent = 12.5;   // one XCD (32 of 256 CUs)
+  int max_timeslice_replicas = 4;
 };
 
-enum class SchedEventType { Scheduled, Failed, Released, Preempted, GangReady, GangTimeout };
+enum class SchedEventType { Scheduled, Failed, Released, Preempted, GangReady, GangTimeout, Migrated };
 struct SchedEvent {
   SchedEventType type;
   std::string uid, node, detail;
@@ -168,7 +196,8 @@ struct SchedulerMetrics {
   uint64_t attempts = 0, scheduled = 0, failed = 0, topology_optimal = 0, preemptions = 0,
            releases = 0, gang_timeouts = 0;
   double avg_latency_ms = 0.0, p50_ms = 0.0, p90_ms = 0.0, p99_ms = 0.0, max_ms = 0.0;
-  size_t active_allocations = 0, allocated_gpus = 0, allocated_partitions = 0;
+  size_t active_allocations = 0, allocated_gpus = 0, allocated_partitions = 0, shared_gpus = 0,
+         share_clients = 0;
 };
 
 class Scheduler {
@@ -191,12 +220,21 @@ class Scheduler {
   std::string permit(const std::string& uid);
 
   bool release(const std::string& uid);
+  // Explicit share placement (SharingManager / tests): a client slot for the
+  // sharing request `w` on GPU `gpu` of `node`.
+  Decision reserve_share(const WorkloadRequest& w, const std::string& node, const std::string& gpu);
+  // Move one partition slice of `uid` to another free slice (consolidation).
+  // Atomic under the ledger lock; false if `to` is no longer free.
+  bool migrate_partition(const std::string& uid, const std::string& from, const std::string& to);
   void expire_gangs();  // release timed-out gang reservations
   // Restore the ledger (controller restart: rebuilt from pod annotations).
   bool restore(const Allocation& a);
 
-  // True when the GPU or any of its partition slices is held in the ledger.
+  // True when the GPU, any of its partition slices or a share of it is held
+  // in the ledger.
   bool gpu_busy(const GpuDevice& g) const;
+  // Share clients currently on a GPU (CoLocate / TimeSlice).
+  int share_clients(const std::string& gpu_uuid) const;
   // Partition-switch fence: atomically (under the ledger lock) check that no
   // whole-GPU or slice reservation holds `gpu_uuid` and bar new ones until
   // unfence_gpu.  Closes the window between the controller's idle check and
@@ -235,7 +273,11 @@ class Scheduler {
                             const WorkloadRequest& w, std::vector<std::string>* sel) const;
   int resource_score(const std::vector<const GpuDevice*>& avail, const WorkloadRequest& w) const;
   int balance_score(const NodeTopology& n, int requested) const;
+  // Sharing requests: best-fit GPU on the node + CU range; false if none.
+  bool pick_share(const NodeTopology& n, const WorkloadRequest& w, NodeScore* s) const;
+  bool share_fits(const GpuDevice& g, const WorkloadRequest& w, int* cu_begin, int* cu_end) const;
   bool reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending);
+  void erase_locked(std::unordered_map<std::string, Allocation>::iterator it);
   bool try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d);
   void emit(SchedEvent e);
   double bandwidth_of(const NodeTopology& n, const std::vector<std::string>& gpus) const;
@@ -247,6 +289,11 @@ class Scheduler {
   std::unordered_map<std::string, Allocation> allocs_;
   std::unordered_map<std::string, std::string> gpu_owner_;   // gpu uuid -> uid
   std::unordered_map<std::string, std::string> part_owner_;  // partition id -> uid
+  struct SharedGpu {
+    SharingMethod method = SharingMethod::None;
+    std::vector<std::string> clients;  // uids
+  };
+  std::unordered_map<std::string, SharedGpu> shared_;        // gpu uuid -> clients
   std::set<std::string> fenced_;                             // GPUs mid partition switch
   mutable std::mutex cordon_mu_;
   std::set<std::string> cordoned_;

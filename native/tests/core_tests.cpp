@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <map>
 #include <random>
+#include <map>
 #include <set>
 #include <string>
 #include <thread>
@@ -71,12 +72,29 @@ static WorkloadRequest slice(const std::string& uid) {
   return w;
 }
 
-// Ledger invariant: every GPU / slice has at most one owner, and no GPU is
-// held whole while any of its slices is held.
+static WorkloadRequest share(const std::string& uid) {
+  WorkloadRequest w;
+  w.uid = w.name = uid;
+  w.gpu_count = 1;
+  w.sharing = SharingMethod::CoLocate;
+  w.share_cu_percent = 12.5;
+  w.share_memory_gb = 30.0;
+  w.type = WorkloadType::Inference;
+  return w;
+}
+
+// Ledger invariant: every GPU / slice has at most one owner, no GPU is held
+// whole while any of its slices is held, a shared GPU is neither held whole
+// nor sliced, and co-located clients of one GPU have disjoint CU ranges.
 static bool ledger_consistent(Scheduler& s, size_t* n_gpus = nullptr) {
   std::set<std::string> seen, whole, sliced;
+  std::map<std::string, std::vector<std::pair<int, int>>> shared;
   size_t total = 0;
   for (const auto& a : s.allocations()) {
+    if (!a.shared_gpu.empty()) {
+      shared[a.shared_gpu].emplace_back(a.cu_begin, a.cu_end);
+      ++total;
+    }
     for (const auto& g : a.gpus) {
       if (!seen.insert(g).second) return false;
       whole.insert(g);
@@ -90,6 +108,12 @@ static bool ledger_consistent(Scheduler& s, size_t* n_gpus = nullptr) {
   }
   for (const auto& g : sliced)
     if (whole.count(g)) return false;
+  for (auto& kv : shared) {
+    if (whole.count(kv.first) || sliced.count(kv.first)) return false;
+    std::sort(kv.second.begin(), kv.second.end());
+    for (size_t i = 1; i < kv.second.size(); ++i)
+      if (kv.second[i].first < kv.second[i - 1].second) return false;  // overlapping CU masks
+  }
   if (n_gpus) *n_gpus = total;
   return true;
 }
@@ -207,8 +231,8 @@ static void test_concurrent_ledger_stress(int threads, int iters) {
       std::vector<std::string> mine;
       for (int i = 0; i < iters; ++i) {
         const std::string uid = "t" + std::to_string(t) + "-" + std::to_string(i);
-        const int kind = static_cast<int>(rng() % 5);
-        WorkloadRequest w = kind == 4 ? slice(uid) : gpus(uid, 1 << (rng() % 3));
+        const int kind = static_cast<int>(rng() % 6);
+        WorkloadRequest w = kind == 4 ? slice(uid) : kind == 5 ? share(uid) : gpus(uid, 1 << (rng() % 3));
         Decision d;
         if (kind == 3) {  // extender path: filter -> bind on the first passing node
           std::vector<std::string> nodes = {"n0", "n1", "n2", "n3"}, passed;
@@ -242,6 +266,13 @@ static void test_concurrent_ledger_stress(int threads, int iters) {
     double now = 0;
     while (!stop.load()) p->tick(now += 1.0);
   });
+  std::thread consolidator([&] {  // moves slices in the ledger under everyone's feet
+    ConsolidationPolicy pol;
+    pol.after_s = 0;
+    pol.cooldown_s = 0;
+    double now = 0;
+    while (!stop.load()) (void)p->partitions()->consolidate(now += 1.0, pol, true);
+  });
   std::thread scraper([&] {
     while (!stop.load()) {
       (void)p->expose_metrics();
@@ -254,6 +285,7 @@ static void test_concurrent_ledger_stress(int threads, int iters) {
   stop = true;
   refresher.join();
   ticker.join();
+  consolidator.join();
   scraper.join();
   size_t held = 0;
   CHECK(violations.load() == 0);

@@ -59,7 +59,7 @@ def test_bench_rank_refuses_mismatched_world():
 
 @pytest.mark.gpu
 def test_bench_gpus1_through_launcher_on_gpu():
-    r, lines = _run(1, ["--model", "llama3.2-1b", "--seq-len", "2048", "--micro-batch", "2"],
+    r, lines = _run(1, ["--model", "llama3-8b", "--seq-len", "2048", "--micro-batch", "1"],
                     timeout=400)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(lines[-1])

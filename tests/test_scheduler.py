@@ -198,8 +198,10 @@ def test_p99_is_a_quantile_not_max():
     for _ in range(1000):
         p.observe_pod_latency_ms(1.0)
     p.observe_pod_latency_ms(5000.0)
-    m = p.scheduler_metrics()
-    assert m["p99_ms"] < 2.0 and m["max_ms"] >= 5000.0
+    # the pod create -> bind histogram (kgwe_scheduling_latency_ms)
+    assert p.pod_latency_quantile_ms(0.99) < 2.0 and p.pod_latency_quantile_ms(0.9999) >= 1000.0
+    assert p.pod_latency_count() == 1001
+    assert "kgwe_scheduling_latency_ms_count 1001" in p.expose_metrics()
 
 
 def test_compat_mode_reproduces_reference_formulas():

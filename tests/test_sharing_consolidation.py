@@ -1,0 +1,263 @@
+"""GPU sharing held in the scheduler ledger, partition consolidation, gangs
+on one xGMI island, pod create -> bind latency recorded by bind itself,
+queue depth, and failover restore of the full ledger entry."""
+import json
+import time
+
+import pytest
+
+from kgwe.core import Platform, make_fixture
+
+
+def share_wl(uid, method="CoLocate", cu=12.5, mem=30.0, prio=0, preemptible=True):
+    return {"metadata": {"name": uid, "namespace": "inf", "uid": uid},
+            "spec": {"workloadType": "Inference", "priority": prio, "preemptible": preemptible,
+                     "gpuRequirements": {"count": 1, "sharing": {"method": method, "cuPercent": cu,
+                                                                  "memoryGB": mem}}}}
+
+
+def whole_wl(uid, n, prio=0, preemptible=True, topo="xGMIOptimal", gang=None):
+    w = {"metadata": {"name": uid, "namespace": "train", "uid": uid},
+         "spec": {"workloadType": "Training", "priority": prio, "preemptible": preemptible,
+                  "gpuRequirements": {"count": n, "topology": {"preference": topo}},
+                  "distributedConfig": {"strategy": "DataParallel"}}}
+    if gang:
+        w["spec"]["gang"] = {"name": gang[0], "size": gang[1]}
+    return w
+
+
+def cpx_wl(uid):
+    return {"metadata": {"name": uid, "namespace": "inf", "uid": uid},
+            "spec": {"workloadType": "Inference",
+                     "gpuRequirements": {"count": 0, "partition": {"mode": "CPX", "count": 1}}}}
+
+
+@pytest.fixture
+def plat():
+    p = Platform({"enforceBudgets": False})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    return p
+
+
+def test_eight_colocated_clients_pack_one_gpu_with_disjoint_xcd_masks(plat):
+    ds = [plat.schedule(share_wl(f"c{i}")) for i in range(8)]
+    assert all(d["ok"] for d in ds)
+    gpus = {d["shared_gpu"] for d in ds}
+    assert len(gpus) == 1  # best fit: one GPU, 8 x one XCD (32 CUs)
+    ranges = sorted((d["cu_begin"], d["cu_end"]) for d in ds)
+    assert ranges == [(32 * i, 32 * i + 32) for i in range(8)]
+    masks = {d["env"]["HSA_CU_MASK"] for d in ds}
+    assert len(masks) == 8 and all(m.startswith("0:") for m in masks)
+    assert all(d["env"]["KGWE_SHARING"] == "CoLocate" for d in ds)
+    assert all(float(d["env"]["KGWE_GPU_MEMORY_FRACTION"]) == pytest.approx(30 / 288, rel=1e-3)
+               for d in ds)
+    # a ninth client opens a second GPU
+    d9 = plat.schedule(share_wl("c8"))
+    assert d9["ok"] and d9["shared_gpu"] not in gpus
+    m = plat.scheduler_metrics()
+    assert m["shared_gpus"] == 2 and m["share_clients"] == 9
+
+
+def test_shared_gpu_is_never_handed_out_whole_or_partitioned(plat):
+    assert plat.schedule(share_wl("s0"))["ok"]
+    shared = plat.allocations()[0]["shared_gpu"]
+    d = plat.schedule(whole_wl("big", 8))  # needs all 8 GPUs: one is shared
+    assert not d["ok"]
+    d7 = plat.schedule(whole_wl("seven", 7))
+    assert d7["ok"] and shared not in d7["gpus"]
+    # the shared GPU is not idle: no partition switch may take it
+    assert plat.ensure_partitions("CPX", 1) == [] or all(
+        op["gpu"] != shared for op in plat.partition_ops())
+    plat.release("seven")
+    # and a whole-GPU holder never takes clients
+    dw = plat.schedule(whole_wl("one", 1))
+    for i in range(8):
+        ds = plat.schedule(share_wl(f"x{i}"))
+        assert ds["ok"] and ds["shared_gpu"] != dw["gpus"][0]
+
+
+def test_timeslice_and_colocate_do_not_mix_on_one_gpu(plat):
+    a = plat.schedule(share_wl("ts0", method="TimeSlice", mem=0))
+    b = plat.schedule(share_wl("co0"))
+    assert a["ok"] and b["ok"] and a["shared_gpu"] != b["shared_gpu"]
+    assert "HSA_CU_MASK" not in a["env"] and a["env"]["KGWE_SHARING"] == "TimeSlice"
+
+
+def test_memory_cap_limits_clients(plat):
+    ds = [plat.schedule(share_wl(f"m{i}", cu=5, mem=100.0)) for i in range(3)]
+    assert all(d["ok"] for d in ds)
+    assert len({d["shared_gpu"] for d in ds}) == 2  # 2 x 100 GB fit 288 GB, the third does not
+
+
+def test_share_release_frees_the_gpu_for_whole_allocation(plat):
+    d = plat.schedule(share_wl("s0"))
+    assert not plat.schedule(whole_wl("all8", 8))["ok"]
+    plat.release("s0")
+    assert plat.schedule(whole_wl("all8", 8))["ok"]
+
+
+def test_share_clients_are_preemptible_victims(plat):
+    for i in range(8):
+        assert plat.schedule(whole_wl(f"w{i}", 1, prio=0))["ok"] or True
+    plat.release("w7")
+    assert plat.schedule(share_wl("s0", prio=1))["ok"]
+    d = plat.schedule(whole_wl("urgent", 1, prio=100, preemptible=False))
+    assert d["ok"] and d["preempted"]
+
+
+def test_extender_pod_with_gpu_shared_resource_gets_cu_mask(plat):
+    pod = {"metadata": {"name": "srv", "namespace": "inf", "uid": "u-srv",
+                        "annotations": {"kgwe.amd.com/cu-percent": "25", "kgwe.amd.com/memory-gb": "36"}},
+           "spec": {"containers": [{"name": "m", "resources": {"limits": {"amd.com/gpu-shared": "1"}}}]}}
+    body = json.dumps({"pod": pod, "nodenames": ["n0"]})
+    f = json.loads(plat.filter(body))
+    assert f["nodenames"] == ["n0"]
+    res = plat.bind(json.dumps({"podName": "srv", "podNamespace": "inf", "podUID": "u-srv", "node": "n0"}))
+    assert res["result"] == {} or not res["result"].get("error")
+    env = res["placement"]["env"]
+    assert env["KGWE_SHARING"] == "CoLocate" and env["HSA_CU_MASK"] == "0:0-63"
+    assert res["placement"]["workload"]["sharing"] == "CoLocate"
+
+
+def test_gang_lands_on_one_xgmi_island():
+    p = Platform({"enforceBudgets": False})
+    for n in ("a", "b", "c"):
+        p.add_fake_node(make_fixture(n, 8, 2))
+    # fragment: 2 GPUs used on a and b each, c half used
+    for i, node_fill in enumerate((2, 2, 4)):
+        for k in range(node_fill):
+            p.schedule(whole_wl(f"f{i}{k}", 1, topo="None"))
+    members = [whole_wl(f"g{k}", 1, gang=("g", 4)) for k in range(4)]
+    ds = p.schedule_gang(members)
+    assert all(d["ok"] for d in ds)
+    assert len({d["node"] for d in ds}) == 1
+    assert len({g for d in ds for g in d["gpus"]}) == 4
+    # xGMIRequired gang larger than any node's free GPUs: refused, nothing held
+    big = [whole_wl(f"h{k}", 5, topo="xGMIRequired", gang=("h", 2)) for k in range(2)]
+    before = len(p.allocations())
+    assert not any(d["ok"] for d in p.schedule_gang(big))
+    assert len(p.allocations()) == before
+
+
+def test_preempting_a_gang_member_preempts_the_whole_gang():
+    p = Platform({"enforceBudgets": False})
+    p.add_fake_node(make_fixture("a", 8, 2))
+    p.add_fake_node(make_fixture("b", 8, 2))
+    # 2 x 5 GPUs cannot share a node: one member per node
+    ds = p.schedule_gang([whole_wl(f"g{k}", 5, prio=1, topo="None", gang=("g", 2)) for k in range(2)])
+    assert all(d["ok"] for d in ds) and len({d["node"] for d in ds}) == 2
+    for n in ("a", "b"):
+        assert p.schedule(whole_wl(f"fill-{n}", 3, prio=1000, preemptible=False, topo="None"))["ok"]
+    d = p.schedule(whole_wl("urgent", 5, prio=500, preemptible=False, topo="None"))
+    assert d["ok"]
+    assert set(d["preempted"]) == {"g0", "g1"}  # both members, even the one on the other node
+    assert not any(a["uid"] in ("g0", "g1") for a in p.allocations())
+
+
+def test_consolidation_empties_underused_cpx_gpus_and_reclaims_them():
+    p = Platform({"enforceBudgets": False, "partitionReclaimIdleSeconds": -1,
+                  "partitionConsolidateAfterSeconds": 0, "migrationCooldownSeconds": 0})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    # 16 slices on 2 CPX GPUs, then free most of them: 3 left on each GPU
+    uids = [f"i{k}" for k in range(16)]
+    for u in uids:
+        assert p.schedule(cpx_wl(u))["ok"]
+    assert p.partition_metrics()["modes"]["CPX"]["gpus"] == 2
+    by_gpu = {}
+    for a in p.allocations():
+        by_gpu.setdefault(a["partitions"][0].rsplit("/p", 1)[0], []).append(a["uid"])
+    keep = []
+    for g, us in by_gpu.items():
+        for u in us[3:]:
+            p.release(u)
+        keep += us[:3]
+    assert p.partition_metrics()["slice_utilization"] == pytest.approx(6 / 16)
+    moves = p.consolidate_partitions(time.time(), plan_only=False)
+    assert len(moves) == 3 and all(m["uid"] in keep for m in moves)
+    m = p.partition_metrics()
+    assert m["modes"]["CPX"]["gpus"] == 1 and m["slice_utilization"] == pytest.approx(6 / 8)
+    assert m["migrations"] == 3
+    # every workload still holds exactly one slice, all on one GPU
+    held = [a["partitions"] for a in p.allocations()]
+    assert len(held) == 6 and all(len(h) == 1 for h in held)
+    assert len({h[0].rsplit("/p", 1)[0] for h in held}) == 1
+
+
+def test_consolidation_never_moves_training_or_nonpreemptible():
+    p = Platform({"enforceBudgets": False, "partitionReclaimIdleSeconds": -1,
+                  "partitionConsolidateAfterSeconds": 0})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    w = cpx_wl("keep")
+    w["spec"]["preemptible"] = False
+    assert p.schedule(w)["ok"]
+    for k in range(9):
+        assert p.schedule(cpx_wl(f"x{k}"))["ok"]
+    for k in range(1, 9):
+        p.release(f"x{k}")
+    # GPU A: keep + x0? (packing order) — whatever the layout, "keep" never moves
+    moves = p.consolidate_partitions(time.time(), plan_only=False)
+    assert all(m["uid"] != "keep" for m in moves)
+
+
+def test_consolidation_hysteresis_waits():
+    p = Platform({"enforceBudgets": False, "partitionReclaimIdleSeconds": -1,
+                  "partitionConsolidateAfterSeconds": 100})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    for k in range(9):
+        p.schedule(cpx_wl(f"x{k}"))
+    for k in range(1, 8):
+        p.release(f"x{k}")
+    assert p.consolidate_partitions(1000.0, plan_only=True) == []
+    assert p.consolidate_partitions(1050.0, plan_only=True) == []
+    assert len(p.consolidate_partitions(1101.0, plan_only=True)) == 1
+
+
+def test_bind_records_pod_latency_and_queue_depth(plat):
+    names = [f"p{i}" for i in range(5)]
+    for n in names:
+        pod = {"metadata": {"name": n, "namespace": "d", "uid": "u-" + n},
+               "spec": {"containers": [{"name": "m", "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+        plat.filter(json.dumps({"pod": pod, "nodenames": ["n0"]}))
+    assert plat.queue_depth() == 5
+    time.sleep(0.02)
+    for n in names:
+        r = plat.bind(json.dumps({"podName": n, "podNamespace": "d", "podUID": "u-" + n, "node": "n0"}))
+        assert not r["result"].get("error")
+    assert plat.queue_depth() == 0
+    assert plat.pod_latency_count() == 5
+    assert plat.pod_latency_quantile_ms(0.5) >= 20.0
+    text = plat.expose_metrics()
+    assert 'kgwe_scheduling_latency_ms_count 5' in text
+    assert 'kgwe_workload_queue_depth 0' in text
+
+
+def test_bind_uses_microsecond_creation_stamp(plat):
+    pod = {"metadata": {"name": "s", "namespace": "d", "uid": "u-s",
+                        "annotations": {"kgwe.amd.com/created-at": f"{time.time() - 0.25:.6f}"}},
+           "spec": {"containers": [{"name": "m", "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+    plat.filter(json.dumps({"pod": pod, "nodenames": ["n0"]}))
+    plat.bind(json.dumps({"podName": "s", "podNamespace": "d", "podUID": "u-s", "node": "n0"}))
+    assert 240.0 <= plat.pod_latency_quantile_ms(0.5) <= 400.0
+
+
+def test_restore_keeps_preemptible_type_gang_and_share():
+    p = Platform({"enforceBudgets": False})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    assert p.restore_allocation({"uid": "nonpre", "node": "n0", "gpus": ["GPU-n0-00"], "priority": 5,
+                                 "preemptible": False, "type": "Training", "gang": "g", "gang_size": 2})
+    assert p.restore_allocation({"uid": "share", "node": "n0", "sharing": "CoLocate",
+                                 "shared_gpu": "GPU-n0-01", "cu_begin": 0, "cu_end": 32,
+                                 "type": "Inference"})
+    a = {x["uid"]: x for x in p.allocations()}
+    assert a["nonpre"]["preemptible"] is False and a["nonpre"]["gang"] == "g"
+    assert a["nonpre"]["gang_size"] == 2 and a["share"]["shared_gpu"] == "GPU-n0-01"
+    assert p.permit("nonpre") == "Allow"
+    # the non-preemptible entry survives a high-priority arrival
+    for i in range(2, 8):
+        p.schedule(whole_wl(f"f{i}", 1, prio=0, topo="None"))
+    d = p.schedule(whole_wl("vip", 8, prio=10_000, topo="None"))
+    assert not d["ok"] or "nonpre" not in d["preempted"]
+    assert any(x["uid"] == "nonpre" for x in p.allocations())
+    # and the restored share still blocks whole-GPU use of its GPU
+    d1 = p.schedule(whole_wl("w1", 1, prio=0, topo="None"))
+    assert not d1["ok"] or "GPU-n0-01" not in d1["gpus"]
