@@ -1,0 +1,154 @@
+"""bf16 Llama decoding on the kgwe HIP kernels (the inference pods the
+platform co-locates / partitions: BASELINE.json config 4, "8 bf16 inference
+pods"; reference README.md:31 "7x GPU density").
+
+* prefill: the training forward's kernels (fused QKV split + RoPE, flash
+  attention at head_dim 128, SDPA otherwise) and a copy of K/V into the
+  cache;
+* decode step: RMSNorm (+residual) -> QKV GEMM -> fused RoPE + KV-cache
+  append (``kgwe_decode_rope_append``) -> split-K GQA decode attention
+  (``kgwe_decode_attn``) -> o-proj -> RMSNorm -> w13 GEMM -> SwiGLU -> w2,
+  greedy argmax; positions advance INSIDE the step, so the whole step is
+  captured once in a hipGraph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm)
+  and replayed — a 1B-parameter decode step is ~200 kernels, launch-bound
+  without a graph.
+
+KV cache: one bf16 tensor [L, B, Hkv, Smax, D] (head-major, so one
+(sequence, kv head) is a contiguous slab the decode kernel streams).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import attn as attn_ops
+from ..ops import decode as dec
+from ..ops import functional as K
+from ..ops import reference as ref
+from .llama import Llama
+
+
+class Generator:
+    def __init__(self, model: Llama, batch: int, max_seq: int, keep_logits: bool = False):
+        self.m = model
+        self.keep_logits = keep_logits
+        self.logits = None
+        c = model.cfg
+        self.cfg = c
+        p = next(model.parameters())
+        self.dev = p.device
+        self.B, self.smax = batch, max_seq
+        hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
+        self.kv = torch.zeros(2, c.n_layers, batch, hkv, max_seq, d, device=self.dev, dtype=p.dtype)
+        self.cos, self.sin = ref.rope_tables(max_seq, d, c.rope_theta, self.dev)
+        self.cos, self.sin = self.cos.float().contiguous(), self.sin.float().contiguous()
+        self.attn = dec.DecodeAttention(batch, hq, hkv, d, max_seq, self.dev)
+        self.tok = torch.zeros(batch, dtype=torch.long, device=self.dev)
+        self.pos = torch.zeros(batch, dtype=torch.int32, device=self.dev)
+        self.lens = torch.zeros(batch, dtype=torch.int32, device=self.dev)
+        self.graph = None
+        self.filled = 0  # host-side count of cached positions (no device sync)
+
+    # ------------------------------------------------------------ prefill
+    @torch.no_grad()
+    def prefill(self, tokens: torch.Tensor) -> torch.Tensor:
+        """tokens [B, P] -> next token [B]; fills cache positions [0, P)."""
+        c, m = self.cfg, self.m
+        B, P = tokens.shape
+        if B != self.B or P >= self.smax:
+            raise ValueError(f"prefill: expected [B={self.B}, P<{self.smax}], got {tuple(tokens.shape)}")
+        hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
+        cos, sin = self.cos[:P], self.sin[:P]
+        h = m.tok_embeddings(tokens)
+        residual = None
+        for i, layer in enumerate(m.layers):
+            if residual is None:
+                xn, residual = K.rmsnorm(h, layer.attention_norm, c.norm_eps)
+            else:
+                xn, residual = K.rmsnorm(h, layer.attention_norm, c.norm_eps, residual=residual)
+            qkv = K.linear(xn, layer.attention.wqkv).view(B * P, -1)
+            q, k, v = K.rope_qkv(qkv, cos, sin, P, hq, hkv, d)
+            k4, v4 = k.view(B, P, hkv, d), v.view(B, P, hkv, d)
+            self.kv[0, i, :, :, :P].copy_(k4.transpose(1, 2))
+            self.kv[1, i, :, :, :P].copy_(v4.transpose(1, 2))
+            o = attn_ops.attention(q.view(B, P, hq, d), k4, v4, causal=True)
+            a = K.linear(o.reshape(B, P, -1), layer.attention.wo)
+            xn, residual = K.rmsnorm(a, layer.ffn_norm, c.norm_eps, residual=residual)
+            h = layer.feed_forward(xn)
+        h, _ = K.rmsnorm(h, m.norm, c.norm_eps, residual=residual)
+        logits = K.linear(h[:, -1], m.output)
+        if self.keep_logits:
+            self.logits = logits.clone()
+        nxt = logits.argmax(-1)
+        self.tok.copy_(nxt)
+        self.pos.fill_(P)
+        self.lens.fill_(P + 1)
+        self.filled = P
+        return nxt
+
+    # ------------------------------------------------------------ decode
+    @torch.no_grad()
+    def _step(self) -> None:
+        c, m = self.cfg, self.m
+        hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
+        h = m.tok_embeddings(self.tok)  # [B, dim]
+        residual = None
+        for i, layer in enumerate(m.layers):
+            if residual is None:
+                xn, residual = K.rmsnorm(h, layer.attention_norm, c.norm_eps)
+            else:
+                xn, residual = K.rmsnorm(h, layer.attention_norm, c.norm_eps, residual=residual)
+            qkv = K.linear(xn, layer.attention.wqkv)
+            q = dec.rope_append(qkv, self.pos, self.cos, self.sin, self.kv[0, i], self.kv[1, i], hq, hkv, d)
+            o = self.attn(q, self.kv[0, i], self.kv[1, i], self.lens)
+            a = K.linear(o.view(self.B, -1), layer.attention.wo)
+            xn, residual = K.rmsnorm(a, layer.ffn_norm, c.norm_eps, residual=residual)
+            h = layer.feed_forward(xn)
+        h, _ = K.rmsnorm(h, m.norm, c.norm_eps, residual=residual)
+        logits = K.linear(h, m.output)
+        if self.keep_logits:  # tests: a static buffer the graph writes every replay
+            if self.logits is None:
+                self.logits = torch.empty_like(logits)
+            self.logits.copy_(logits)
+        self.tok.copy_(logits.argmax(-1))
+        self.pos.add_(1)
+        self.lens.add_(1)
+
+    def capture(self) -> None:
+        """Record one decode step in a hipGraph (warm-up on a side stream, as
+        graph capture requires).  Positions advance inside the graph."""
+        if self.dev.type != "cuda":
+            return
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        saved = (self.tok.clone(), self.pos.clone(), self.lens.clone())
+        with torch.cuda.stream(s):
+            self._step()  # allocator warm-up, lazy library handles
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        self.tok.copy_(saved[0])
+        self.pos.copy_(saved[1])
+        self.lens.copy_(saved[2])
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step()
+        self.graph = g
+        # capture does not execute the work: state is unchanged
+
+    def step(self) -> torch.Tensor:
+        if self.filled + 1 >= self.smax:
+            raise RuntimeError("KV cache full")
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step()
+        self.filled += 1
+        return self.tok
+
+    @torch.no_grad()
+    def generate(self, prompt: torch.Tensor, new_tokens: int, graph: bool = True) -> torch.Tensor:
+        self.prefill(prompt)
+        if graph and self.graph is None:
+            self.capture()
+        out = [self.tok.clone()]
+        for _ in range(new_tokens - 1):
+            out.append(self.step().clone())
+        return torch.stack(out, 1)

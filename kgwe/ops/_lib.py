@@ -46,6 +46,12 @@ _SIGS = {
                                 c_float, c_int, c_float, c_void_p]),
     "kgwe_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
     "kgwe_adamw_chunk_elems": (c_int, []),
+    "kgwe_decode_rope_append": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "kgwe_decode_attn": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                 c_int, c_int, c_int, c_int, c_int, c_float, c_void_p]),
+    "kgwe_decode_attn_workspace": (c_int64, [c_int, c_int, c_int, c_int]),
+    "kgwe_decode_attn_splits": (c_int, [c_int, c_int, c_int]),
     "kgwe_adamw_tensor_bytes": (c_int, []),
 }
 _OPTIONAL_SIGS = {

@@ -615,6 +615,11 @@ std::map<std::string, std::string> share_env(SharingMethod m, int gpu_index, int
     env["HSA_CU_MASK"] = "0:" + std::to_string(cu_begin) + "-" + std::to_string(cu_end - 1);
     env["KGWE_CU_RANGE"] = std::to_string(cu_begin) + "-" + std::to_string(cu_end);
   }
+  // Measured on MI355X (profiles/r02_colocate): co-located processes run
+  // concurrently only while each holds <= 2 hardware queues; at the HIP
+  // default (4) the scheduler time-slices the clients' queues and 8 clients
+  // together decode 3-5x slower than ONE client alone.
+  if (m == SharingMethod::CoLocate || m == SharingMethod::TimeSlice) env["GPU_MAX_HW_QUEUES"] = "2";
   if (memory_gb > 0 && gpu_memory_gb > 0) {
     char buf[32];
     std::snprintf(buf, sizeof buf, "%.4f", std::min(1.0, memory_gb / gpu_memory_gb));

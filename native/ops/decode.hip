@@ -1,0 +1,265 @@
+// Decode-time (one new token per sequence) kernels for the bf16 inference
+// harness: fused RoPE + KV-cache append, and split-K GQA attention over the
+// cache ("flash decoding"), written for 64-lane CDNA4 wavefronts.
+//
+// Layouts
+//   qkv     [B, (Hq + 2*Hkv) * D]  fused projection output of the new token
+//   pos     [B] int32              position of the new token (= tokens cached)
+//   k/v cache [B, Hkv, Smax, D]    bf16, head-major so one (b, kv-head) is a
+//                                  contiguous [Smax, D] slab
+//   q       [B, Hq, D]; out [B, Hq, D]
+//
+// Decode attention is HBM-bound (every cached K/V byte is read once per
+// step) and has little parallelism per sequence, so the key range of each
+// (sequence, kv-head) is split into `splits` chunks that run as separate
+// workgroups; a second kernel merges the partial softmax states.  One
+// workgroup serves ALL G = Hq/Hkv query heads of its kv-head (one wave per
+// query head), so each K/V tile is read from HBM once and reused G times
+// from LDS.  The split count depends only on the cache capacity, so a
+// decode step can be captured once in a hipGraph and replayed at any length.
+#include <algorithm>
+
+#include "common.h"
+
+using namespace kgwe;
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+// ---------------------------------------------------------------------------
+// RoPE of q and k for the new token at pos[b] + append of k, v to the cache.
+// One thread = one 8-wide chunk of the first half of one head plus the
+// matching chunk of the second half ("rotate_half" convention, as rope.hip).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_append_kernel(
+    const bf16_t* __restrict__ qkv, const int* __restrict__ pos, const float* __restrict__ cosT,
+    const float* __restrict__ sinT, bf16_t* __restrict__ q_out, bf16_t* __restrict__ kc,
+    bf16_t* __restrict__ vc, int B, int Hq, int Hkv, int D, int Smax) {
+  const int half = D / 2;
+  const int cpp = half / 8;
+  const int Ht = Hq + 2 * Hkv;
+  const int64_t n = static_cast<int64_t>(B) * Ht * cpp;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += gridDim.x * 256LL) {
+    const int b = static_cast<int>(i / (static_cast<int64_t>(Ht) * cpp));
+    const int rem = static_cast<int>(i - static_cast<int64_t>(b) * Ht * cpp);
+    const int head = rem / cpp;
+    const int c = (rem - head * cpp) * 8;
+    const int p = pos[b];
+    if (p < 0 || p >= Smax) continue;  // never write outside the cache
+    const bf16_t* in = qkv + static_cast<int64_t>(b) * Ht * D + static_cast<int64_t>(head) * D;
+    bf16_t* out;
+    bool rotate = true;
+    if (head < Hq) {
+      out = q_out + (static_cast<int64_t>(b) * Hq + head) * D;
+    } else if (head < Hq + Hkv) {
+      out = kc + ((static_cast<int64_t>(b) * Hkv + (head - Hq)) * Smax + p) * D;
+    } else {
+      out = vc + ((static_cast<int64_t>(b) * Hkv + (head - Hq - Hkv)) * Smax + p) * D;
+      rotate = false;
+    }
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(in + c);
+    const bf16x8 bb = *reinterpret_cast<const bf16x8*>(in + half + c);
+    if (!rotate) {
+      *reinterpret_cast<bf16x8*>(out + c) = a;
+      *reinterpret_cast<bf16x8*>(out + half + c) = bb;
+      continue;
+    }
+    const f32x4* cp = reinterpret_cast<const f32x4*>(cosT + static_cast<int64_t>(p) * half + c);
+    const f32x4* sp = reinterpret_cast<const f32x4*>(sinT + static_cast<int64_t>(p) * half + c);
+    const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+    bf16x8 oa, ob;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cs = j < 4 ? c0[j & 3] : c1[j & 3];
+      const float sn = j < 4 ? s0[j & 3] : s1[j & 3];
+      const float x0 = bf2f(a[j]), x1 = bf2f(bb[j]);
+      oa[j] = f2bf(x0 * cs - x1 * sn);
+      ob[j] = f2bf(x1 * cs + x0 * sn);
+    }
+    *reinterpret_cast<bf16x8*>(out + c) = oa;
+    *reinterpret_cast<bf16x8*>(out + half + c) = ob;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Split-K decode attention.  grid = (splits, Hkv, B), block = 64 * G: wave g
+// owns query head kvh * G + g.  Per 64-key tile: the whole workgroup stages
+// K and V in LDS (16 B vector loads, rows padded by 8 bf16 against bank
+// conflicts); lane j of every wave scores key j against its head (q read
+// from LDS as a broadcast); online softmax in the exp2 domain (q pre-scaled
+// by softmax_scale * log2 e); then lane d accumulates sum_j p_j V[j][d].
+// ---------------------------------------------------------------------------
+template <int D, int G>
+__global__ __launch_bounds__(64 * G) void decode_attn_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ lens, float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv,
+    int Smax, int splits, int chunk, float qscale) {
+  constexpr int kPad = D + 8;
+  constexpr int kPer = D / 64;  // output elements per lane
+  __shared__ __attribute__((aligned(16))) float qs[G][D];
+  __shared__ __attribute__((aligned(16))) bf16_t ks[64][kPad];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[64][kPad];
+  __shared__ float ps[G][64];
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const int Hq = Hkv * G;
+  const int h = kvh * G + wave;
+  const int len = min(lens[b], Smax);
+  const int start = split * chunk;
+  const int end = min(len, start + chunk);
+  const bf16_t* qrow = q + (static_cast<int64_t>(b) * Hq + h) * D;
+#pragma unroll
+  for (int t = 0; t < kPer; ++t) qs[wave][lane + 64 * t] = bf2f(qrow[lane + 64 * t]) * qscale;
+  const int64_t slab = (static_cast<int64_t>(b) * Hkv + kvh) * Smax * D;
+  const bf16_t* kbase = kc + slab;
+  const bf16_t* vbase = vc + slab;
+  float m = -INFINITY, l = 0.0f;
+  float acc[kPer];
+#pragma unroll
+  for (int t = 0; t < kPer; ++t) acc[t] = 0.0f;
+  for (int t0 = start; t0 < end; t0 += 64) {
+    __syncthreads();  // qs written / previous tile consumed
+    constexpr int kChunks = 64 * D / 8;
+    for (int idx = threadIdx.x; idx < kChunks; idx += 64 * G) {
+      const int r = idx / (D / 8), c = (idx % (D / 8)) * 8;
+      const int key = t0 + r;
+      bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < end) {
+        kv = *reinterpret_cast<const bf16x8*>(kbase + static_cast<int64_t>(key) * D + c);
+        vv = *reinterpret_cast<const bf16x8*>(vbase + static_cast<int64_t>(key) * D + c);
+      }
+      *reinterpret_cast<bf16x8*>(&ks[r][c]) = kv;
+      *reinterpret_cast<bf16x8*>(&vs[r][c]) = vv;
+    }
+    __syncthreads();
+    const int key = t0 + lane;
+    float s = -INFINITY;
+    if (key < end) {
+      float d0 = 0.0f, d1 = 0.0f;
+#pragma unroll
+      for (int c = 0; c < D; c += 8) {
+        const bf16x8 kv = *reinterpret_cast<const bf16x8*>(&ks[lane][c]);
+        const f32x4 qa = *reinterpret_cast<const f32x4*>(&qs[wave][c]);
+        const f32x4 qb = *reinterpret_cast<const f32x4*>(&qs[wave][c + 4]);
+        d0 += qa[0] * bf2f(kv[0]) + qa[1] * bf2f(kv[1]) + qa[2] * bf2f(kv[2]) + qa[3] * bf2f(kv[3]);
+        d1 += qb[0] * bf2f(kv[4]) + qb[1] * bf2f(kv[5]) + qb[2] * bf2f(kv[6]) + qb[3] * bf2f(kv[7]);
+      }
+      s = d0 + d1;
+    }
+    const float m_new = fmaxf(m, wave_max(s));  // finite: the tile has >= 1 valid key
+    const float p = key < end ? exp2f(s - m_new) : 0.0f;
+    const float alpha = exp2f(m - m_new);
+    l = l * alpha + wave_sum(p);
+    m = m_new;
+    ps[wave][lane] = p;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) acc[t] *= alpha;
+    const int nkeys = min(64, end - t0);
+    for (int j = 0; j < nkeys; ++j) {
+      const float pj = ps[wave][j];
+#pragma unroll
+      for (int t = 0; t < kPer; ++t) acc[t] += pj * bf2f(vs[j][lane + 64 * t]);
+    }
+  }
+  const int64_t row = (static_cast<int64_t>(b) * Hq + h) * splits + split;
+#pragma unroll
+  for (int t = 0; t < kPer; ++t) part_o[row * D + lane + 64 * t] = acc[t];
+  if (lane == 0) {
+    part_ml[row * 2] = m;
+    part_ml[row * 2 + 1] = l;
+  }
+}
+
+// Merge the per-split softmax states of one (b, h): one wave, lane d.
+template <int D>
+__global__ __launch_bounds__(64) void decode_combine_kernel(const float* __restrict__ part_o,
+                                                            const float* __restrict__ part_ml,
+                                                            bf16_t* __restrict__ out, int splits) {
+  constexpr int kPer = D / 64;
+  const int64_t bh = blockIdx.x;
+  const int lane = threadIdx.x;
+  float M = -INFINITY;
+  for (int s = 0; s < splits; ++s) M = fmaxf(M, part_ml[(bh * splits + s) * 2]);
+  float L = 0.0f, o[kPer];
+#pragma unroll
+  for (int t = 0; t < kPer; ++t) o[t] = 0.0f;
+  if (M > -INFINITY) {
+    for (int s = 0; s < splits; ++s) {
+      const float ms = part_ml[(bh * splits + s) * 2];
+      if (ms == -INFINITY) continue;  // empty split (beyond the sequence)
+      const float w = exp2f(ms - M);
+      L += w * part_ml[(bh * splits + s) * 2 + 1];
+#pragma unroll
+      for (int t = 0; t < kPer; ++t) o[t] += w * part_o[(bh * splits + s) * D + lane + 64 * t];
+    }
+  }
+  const float inv = L > 0.0f ? 1.0f / L : 0.0f;
+#pragma unroll
+  for (int t = 0; t < kPer; ++t) out[bh * D + lane + 64 * t] = f2bf(o[t] * inv);
+}
+
+template <int D, int G>
+int launch_attn(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* lens, float* po,
+                float* pml, bf16_t* out, int B, int Hkv, int Smax, int splits, float scale,
+                hipStream_t st) {
+  const int chunk = ((Smax + splits - 1) / splits + 63) / 64 * 64;
+  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(splits, Hkv, B), dim3(64 * G), 0, st, q, kc,
+                     vc, lens, po, pml, Hkv, Smax, splits, chunk, scale * kLog2e);
+  hipLaunchKernelGGL((decode_combine_kernel<D>), dim3(B * Hkv * G), dim3(64), 0, st, po, pml, out,
+                     splits);
+  return KGWE_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+KGWE_API int kgwe_decode_rope_append(const void* qkv, const int* pos, const float* cos_t,
+                                     const float* sin_t, void* q_out, void* kcache, void* vcache,
+                                     int B, int Hq, int Hkv, int D, int Smax, hipStream_t st) {
+  if (B <= 0 || Hq <= 0 || Hkv <= 0 || D % 16 != 0 || D > 256 || Smax <= 0) return -1;
+  const int64_t n = static_cast<int64_t>(B) * (Hq + 2 * Hkv) * (D / 16);
+  const int grid = static_cast<int>(std::min<int64_t>((n + 255) / 256, 4096));
+  hipLaunchKernelGGL(rope_append_kernel, dim3(grid), dim3(256), 0, st,
+                     static_cast<const bf16_t*>(qkv), pos, cos_t, sin_t, static_cast<bf16_t*>(q_out),
+                     static_cast<bf16_t*>(kcache), static_cast<bf16_t*>(vcache), B, Hq, Hkv, D, Smax);
+  return KGWE_CHECK_LAUNCH();
+}
+
+// Workspace floats: B * Hq * splits * (D + 2).
+KGWE_API int64_t kgwe_decode_attn_workspace(int B, int Hq, int D, int splits) {
+  return static_cast<int64_t>(B) * Hq * splits * (D + 2);
+}
+
+// Split count for a cache of Smax keys: enough workgroups to cover the 256
+// CUs about twice, at least 64 keys per split.
+KGWE_API int kgwe_decode_attn_splits(int B, int Hkv, int Smax) {
+  const int want = (512 + B * Hkv - 1) / (B * Hkv);
+  const int most = (Smax + 63) / 64;
+  return std::max(1, std::min(want, most));
+}
+
+KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vcache, const int* lens,
+                              float* workspace, void* out, int B, int Hq, int Hkv, int D, int Smax,
+                              int splits, float scale, hipStream_t st) {
+  if (B <= 0 || Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || Smax <= 0) return -1;
+  const int G = Hq / Hkv;
+  float* po = workspace;
+  float* pml = workspace + static_cast<int64_t>(B) * Hq * splits * D;
+  auto qp = static_cast<const bf16_t*>(q);
+  auto kp = static_cast<const bf16_t*>(kcache);
+  auto vp = static_cast<const bf16_t*>(vcache);
+  auto op = static_cast<bf16_t*>(out);
+#define KGWE_DECODE_CASE(DD, GG) \
+  if (D == DD && G == GG) return launch_attn<DD, GG>(qp, kp, vp, lens, po, pml, op, B, Hkv, Smax, splits, scale, st);
+  KGWE_DECODE_CASE(64, 1)
+  KGWE_DECODE_CASE(64, 2)
+  KGWE_DECODE_CASE(64, 4)
+  KGWE_DECODE_CASE(64, 8)
+  KGWE_DECODE_CASE(128, 1)
+  KGWE_DECODE_CASE(128, 2)
+  KGWE_DECODE_CASE(128, 4)
+  KGWE_DECODE_CASE(128, 8)
+#undef KGWE_DECODE_CASE
+  return -2;  // unsupported (head_dim, group) combination
+}
