@@ -33,17 +33,22 @@ import urllib.parse
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 from .. import core
+from ..utils import amdsmi_util
 from ..utils.config import load_config
 
 DEFAULTS = {
     "nodeName": "",
     "controllerUrl": "",
+    "advertise": "",  # host:port of this agent's gRPC, pushed with the topology
     "fixture": "",
     "listen": {"host": "0.0.0.0", "port": 9400},
     "grpc": {"enabled": True, "port": 50052},
     "intervalSeconds": 5.0,
     "probe": {"hbm": True, "xgmi": True, "bytesMB": 1024, "iters": 5, "degradedRatio": 0.7},
-    "partition": {"dryRun": True},
+    # Actuation is privileged (amd-smi set_gpu_compute/memory_partition): a
+    # request must carry the controller's bearer token (a Secret mounted into
+    # both pods) and the GPU must be idle on THIS node (no process on it).
+    "partition": {"dryRun": True, "authTokenFile": ""},
 }
 
 
@@ -132,7 +137,10 @@ class NodeAgent:
         u = urllib.parse.urlparse(url)
         try:
             c = http.client.HTTPConnection(u.hostname, u.port or 80, timeout=5)
-            c.request("POST", f"/v1/nodes/{self.name}/topology", body=json.dumps(self.topology),
+            body = dict(self.topology)
+            if self.cfg.get("advertise"):  # where the controller reaches this agent's gRPC
+                body["agent_endpoint"] = self.cfg["advertise"]
+            c.request("POST", f"/v1/nodes/{self.name}/topology", body=json.dumps(body),
                       headers={"Content-Type": "application/json"})
             ok = c.getresponse().status == 200
         except OSError:
@@ -183,8 +191,10 @@ class NodeAgent:
                 n = int(self.headers.get("Content-Length") or 0)
                 body = json.loads(self.rfile.read(n) or b"{}")
                 if self.path.startswith("/v1/partition"):
-                    res = agent.set_partition(body)
-                    return self._send(409 if res.get("error") else 200, json.dumps(res).encode())
+                    auth = self.headers.get("Authorization", "")
+                    res = agent.set_partition(body, auth[7:] if auth.startswith("Bearer ") else "")
+                    code = 403 if res.get("denied") else 409 if res.get("error") else 200
+                    return self._send(code, json.dumps(res).encode())
                 return self._send(404, b"{}")
 
         srv = ThreadingHTTPServer((self.cfg["listen"]["host"], int(self.cfg["listen"]["port"])), H)
@@ -192,13 +202,38 @@ class NodeAgent:
         threading.Thread(target=srv.serve_forever, daemon=True).start()
         return srv
 
-    def set_partition(self, body: dict) -> dict:
-        """Compute / memory partition actuation (dry-run unless configured)."""
+    def _token(self) -> str:
+        path = self.cfg["partition"].get("authTokenFile") or ""
+        if not path:
+            return ""
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return ""
+
+    def set_partition(self, body: dict, token: str = "") -> dict:
+        """Compute / memory partition actuation (dry-run unless configured).
+        Refused without the controller's token, and on a GPU that runs any
+        process (the scheduler's idle check + fence cover its own ledger; this
+        guards against a caller that bypasses it)."""
+        import hmac  # noqa: PLC0415
+
         if not body.get("gpu"):
             return {"error": "gpu required"}
+        want = self._token()
         dry = body.get("dryRun", self.cfg["partition"]["dryRun"]) or self.cfg["partition"]["dryRun"]
+        if not dry:
+            if not want:
+                return {"error": "actuation disabled: partition.authTokenFile is not configured",
+                        "denied": True}
+            if not token or not hmac.compare_digest(token, want):
+                return {"error": "unauthorized", "denied": True}
         if dry:
             return {"dryRun": True, "planned": body}
+        procs = amdsmi_util.gpu_processes_by_uuid(body["gpu"])
+        if procs:
+            return {"error": f"gpu {body['gpu']} busy: {len(procs)} process(es) running"}
         err = core.native.amdsmi_set_partition(body["gpu"], body.get("compute", ""), body.get("memory", ""))
         return {"error": err} if err else {"applied": body}
 

@@ -57,14 +57,20 @@ class AgentService:
     def GetProbes(self, req: dict) -> dict:
         return {"node": self.agent.name, "probes": self.agent.probe_results}
 
-    def SetPartition(self, req: dict) -> dict:
-        return self.agent.set_partition(req)
+    def SetPartition(self, req: dict, ctx=None) -> dict:
+        token = ""
+        if ctx is not None:
+            md = dict(ctx.invocation_metadata() or ())
+            auth = md.get("authorization", "")
+            token = auth[7:] if auth.startswith("Bearer ") else ""
+        return self.agent.set_partition(req, token)
 
 
 def serve(agent, port: int = 50052, host: str = "0.0.0.0", workers: int = 4):
     svc = AgentService(agent)
     handlers = {m: grpc.unary_unary_rpc_method_handler(
-        (lambda m: lambda req, ctx: getattr(svc, m)(req))(m),
+        (lambda m: (lambda req, ctx: svc.SetPartition(req, ctx)) if m == "SetPartition"
+         else (lambda req, ctx: getattr(svc, m)(req)))(m),
         request_deserializer=_de, response_serializer=_ser) for m in METHODS}
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers))
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
@@ -80,8 +86,9 @@ class AgentClient:
         self._stubs = {m: self.channel.unary_unary(f"/{SERVICE}/{m}", request_serializer=_ser,
                                                    response_deserializer=_de) for m in METHODS}
 
-    def call(self, method: str, request: dict | None = None) -> dict:
-        return self._stubs[method](request or {}, timeout=self.timeout)
+    def call(self, method: str, request: dict | None = None, token: str = "") -> dict:
+        md = (("authorization", f"Bearer {token}"),) if token else None
+        return self._stubs[method](request or {}, timeout=self.timeout, metadata=md)
 
     def close(self):
         self.channel.close()

@@ -59,6 +59,17 @@ GPUWORKLOAD_SPEC = _S(
                 "mode": _S(type="string", enum=PARTITION_MODES),
                 "memoryMode": _S(type="string", enum=["NPS1", "NPS2"], default="NPS1"),
                 "count": _S(type="integer", minimum=1, maximum=64, default=1)}),
+            "sharing": _S(type="object", description=(
+                "Share ONE whole SPX GPU with other workloads instead of owning it (reference MPS / "
+                "time-slicing, src/sharing/mig_controller.go:545-857). CoLocate: a disjoint range of "
+                "compute units (HSA_CU_MASK, rounded to whole XCDs) + an HBM cap; TimeSlice: the "
+                "whole GPU, time-shared. The scheduler ledger never hands a shared GPU out whole "
+                "or partitions it. Requires count 1."),
+                properties={"method": _S(type="string", enum=["CoLocate", "TimeSlice", "MPS"],
+                                         default="CoLocate"),
+                            "cuPercent": _S(type="number", minimum=0, maximum=100,
+                                            description="Share of the GPU's 256 CUs (12.5 = one XCD)"),
+                            "memoryGB": _S(type="number", minimum=0, maximum=288)}),
             "mig": _S(type="object", description="Deprecated: mapped to partition",
                       properties={"profile": _S(type="string"), "count": _S(type="integer", minimum=1)}),
             "gpuModel": _S(type="string", description="e.g. MI355X"),
@@ -70,6 +81,8 @@ GPUWORKLOAD_SPEC = _S(
             "strategy": _S(type="string", enum=STRATEGIES),
             "worldSize": _S(type="integer", minimum=1),
             "backend": _S(type="string", enum=BACKENDS, default="RCCL")}),
+        "modelParamsBillions": _S(type="number", minimum=0,
+                                  description="Model size hint for the optimizer's rightsizing"),
         "priority": _S(type="integer", minimum=0, maximum=1000000, default=0),
         "preemptible": _S(type="boolean", default=True),
         "team": _S(type="string"),
@@ -108,7 +121,14 @@ GPUWORKLOAD_STATUS = _S(type="object", properties={
     "startTime": _S(type="string", format="date-time"),
     "completionTime": _S(type="string", format="date-time"),
     "restarts": _S(type="integer", minimum=0),
+    "recoveryRestarts": _S(type="integer", minimum=0),
+    "migrations": _S(type="integer", minimum=0),
     "lastFailure": _S(type="string"),
+    "recommendation": _S(type="object", description="Workload optimizer rightsizing", properties={
+        "gpus": _S(type="integer"), "memoryGB": _S(type="integer"), "partition": _S(type="string"),
+        "expectedUtilization": _S(type="number"), "confidence": _S(type="number"),
+        "costPerHour": _S(type="number"), "reasoning": _S(type="array", items=_S(type="string")),
+        "updated": _S(type="string")}),
     "cost": _S(type="number")})
 
 PARTITIONSTRATEGY_SPEC = _S(type="object", required=["profileDistribution"], properties={
@@ -270,6 +290,8 @@ def validate(obj: dict) -> list[str]:
             errors.append("spec.gpuRequirements: count must be >= 1 unless partition slices are requested")
         if req.get("count", 0) > 0 and req.get("partition"):
             errors.append("spec.gpuRequirements: request whole GPUs or partition slices, not both")
+        if req.get("sharing") and (req.get("count", 0) != 1 or req.get("partition")):
+            errors.append("spec.gpuRequirements.sharing: requires count 1 and no partition")
         dc = spec.get("distributedConfig", {})
         ws = dc.get("worldSize")
         if ws and req.get("count", 0) and ws < req["count"]:

@@ -35,11 +35,12 @@ DEFAULTS = {
     "autoProvisionPartitions": True,
     "partitionReclaimIdleSeconds": 60.0,
     "enforceBudgets": True,
-    "optimizer": {"target": "", "inProcess": True, "learn": True},
+    "optimizer": {"target": "", "inProcess": True, "learn": True, "recommendEverySeconds": 30.0},
     "partitionConsolidation": True,
     "partitionConsolidateBelow": 0.75,
     "partitionConsolidateAfterSeconds": 120.0,
     "migrationCooldownSeconds": 3600.0,
+    "agentActuation": {"enabled": True, "tokenFile": "/etc/kgwe/actuation/token", "timeoutSeconds": 30.0},
     "fakeNodes": 0,
     "labelNodes": True,
     "tickSeconds": 5.0,
@@ -62,11 +63,45 @@ def build(cfg: dict):
         kube = KubeClient(cfg["kube"]["url"], insecure=cfg["kube"]["insecure"])
 
     labeler = NodeLabeler(kube) if kube is not None and cfg["labelNodes"] else None
+    endpoints: dict[str, str] = {}  # node -> agent gRPC host:port (from its pushes)
+    agents: dict[str, object] = {}
+
+    def token() -> str:
+        path = cfg["agentActuation"]["tokenFile"]
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return ""
+
+    def actuate(node: str, gpu: str, compute: str, memory: str) -> str:
+        """Partition switch on an agent-pushed node: the agent's SetPartition,
+        with the bearer token (the agent also refuses a GPU that runs anything)."""
+        ep = endpoints.get(node)
+        if not ep:
+            return f"no agent endpoint known for node {node}"
+        try:
+            from ..agent.grpc_service import AgentClient  # noqa: PLC0415
+
+            c = agents.get(ep)
+            if c is None:
+                c = agents[ep] = AgentClient(ep, timeout=float(cfg["agentActuation"]["timeoutSeconds"]))
+            r = c.call("SetPartition", {"gpu": gpu, "compute": compute, "memory": memory}, token=token())
+        except Exception as e:  # noqa: BLE001 - a failed op, not a crashed extender
+            return f"agent {ep}: {e}"
+        if r.get("error"):
+            return f"agent {ep}: {r['error']}"
+        return ""
+
+    if cfg["agentActuation"]["enabled"]:
+        plat.set_partition_actuator(actuate)
 
     def agent_push(path, body):
         node = json.loads(body)
         name = path.rstrip("/").split("/")[-2]  # /v1/nodes/<name>/topology
         node["name"] = name
+        if node.get("agent_endpoint"):
+            endpoints[name] = node["agent_endpoint"]
         plat.upsert_node(node)
         if labeler is not None:
             try:
@@ -91,7 +126,8 @@ def build(cfg: dict):
 
         optimizer = OptimizerService(learn=bool(cfg["optimizer"]["learn"]))
     rec = (Reconciler(plat, kube, optimizer=optimizer, tick_s=float(cfg["tickSeconds"]),
-                      consolidate=bool(cfg["partitionConsolidation"])) if kube else None)
+                      consolidate=bool(cfg["partitionConsolidation"]),
+                      recommend_every_s=float(cfg["optimizer"]["recommendEverySeconds"])) if kube else None)
     return plat, ext, rec
 
 

@@ -77,6 +77,8 @@ def pod_for_workload(gw: dict, restart: int = 0) -> dict:
         pod_spec["priority"] = int(spec["priority"])
     if req.get("partition"):
         res = {f"amd.com/gpu-{req['partition']['mode'].lower()}": str(req["partition"].get("count", 1))}
+    elif req.get("sharing"):
+        res = {"amd.com/gpu-shared": "1"}
     else:
         res = {"amd.com/gpu": str(req.get("count", 1))}
     c0 = pod_spec["containers"][0]
@@ -108,7 +110,7 @@ def pod_for_workload(gw: dict, restart: int = 0) -> dict:
 
 class Reconciler:
     def __init__(self, platform, kube: KubeClient, optimizer=None, tick_s: float = 5.0,
-                 consolidate: bool = True):
+                 consolidate: bool = True, recommend_every_s: float = RECOMMEND_EVERY_S):
         self.p = platform
         self.kube = kube
         self.optimizer = optimizer
@@ -118,6 +120,7 @@ class Reconciler:
         self.migrations = 0
         self._running: dict[str, tuple] = {}  # pod uid -> (ns, gpuworkload, bound at)
         self._next_recommend = 0.0
+        self.recommend_every_s = recommend_every_s
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._strategy_next: dict[str, float] = {}
@@ -577,7 +580,7 @@ class Reconciler:
                 agg["memory_used_bytes"] = sum(x["memory_used_bytes"] for x in samples) // n
                 self.optimizer.IngestTelemetry({"workload_id": f"{run[0]}/{run[1]}", "samples": [agg]})
         if now >= self._next_recommend:
-            self._next_recommend = now + RECOMMEND_EVERY_S
+            self._next_recommend = now + self.recommend_every_s
             for uid, (ns, wl, _) in list(self._running.items()):
                 try:
                     gw = self.kube.get_cr("GPUWorkload", ns, wl)

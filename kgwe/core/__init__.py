@@ -165,6 +165,12 @@ class Platform:
         hysteresis reclaim, with an explicit clock — simulations)."""
         return _j(self._p.reclaim_idle_after(now, min_idle_s))
 
+    def set_partition_actuator(self, fn) -> None:
+        """fn(node, gpu, compute, memory) -> "" | error: how partition switches
+        reach agent-pushed nodes (the controller's authenticated call to the
+        node agent's SetPartition)."""
+        self._p.set_partition_actuator(fn)
+
     def consolidate_partitions(self, now: float | None = None, plan_only: bool = True) -> list:
         """Consolidating rebalance of partitioned GPUs: list of slice moves
         {uid, from, to, node_from, node_to}.  plan_only=True (controller): the

@@ -42,6 +42,10 @@ class WorkloadType(Enum):
     DATA_PREPROCESSING = "DataPreprocessing"
     REINFORCEMENT = "Reinforcement"
     VISUALIZATION = "Visualization"
+    # GPUWorkload CRD types the reference's optimizer enum lacks
+    BATCH = "Batch"
+    INTERACTIVE = "Interactive"
+    DEVELOPMENT = "Development"
 
 
 class MLFramework(Enum):
@@ -50,6 +54,8 @@ class MLFramework(Enum):
     JAX = "JAX"
     MXNET = "MXNet"
     TRITON = "Triton"
+    VLLM = "vLLM"
+    SGLANG = "SGLang"
 
 
 class DistributionStrategy(Enum):
@@ -277,7 +283,9 @@ class ResourcePredictor:
         (70, 180): (16, 80, True), (180, 500): (32, 80, True),
     }
     FRAMEWORK_OVERHEAD = {MLFramework.PYTORCH: 1.0, MLFramework.TENSORFLOW: 1.1,
-                          MLFramework.JAX: 0.95, MLFramework.TRITON: 0.8}
+                          MLFramework.JAX: 0.95, MLFramework.TRITON: 0.8,
+                          # serving engines size their KV-cache pool to what they are given
+                          MLFramework.VLLM: 1.0, MLFramework.SGLANG: 1.0}
     STRATEGY_EFFICIENCY = {DistributionStrategy.DATA_PARALLEL: 0.85,
                            DistributionStrategy.MODEL_PARALLEL: 0.75,
                            DistributionStrategy.PIPELINE_PARALLEL: 0.80,

@@ -76,6 +76,25 @@ def handle_for_torch_device(index: int):
     return hs[index] if index < len(hs) else None
 
 
+def gpu_processes_by_uuid(uuid: str) -> list:
+    """Processes holding the GPU whose amd-smi uuid / kgwe id is ``uuid`` ([] when
+    amd-smi is unavailable or the GPU is unknown)."""
+    smi = _load()
+    if smi is None:
+        return []
+    for h in gpu_handles():
+        try:
+            u = smi.amdsmi_get_gpu_device_uuid(h)
+        except Exception:  # noqa: BLE001
+            continue
+        if uuid in (u, f"GPU-{u}") or uuid.endswith(str(u)):
+            try:
+                return list(smi.amdsmi_get_gpu_process_list(h) or [])
+            except Exception:  # noqa: BLE001
+                return []
+    return []
+
+
 def gfx_activity(handle) -> float | None:
     smi = _load()
     if smi is None or handle is None:

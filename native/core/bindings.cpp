@@ -3,6 +3,7 @@
 // The boundary is JSON text both ways, so the shells never hold C++ objects
 // beyond the Platform handle and the GIL is released for every hot call.
 #include <pybind11/pybind11.h>
+#include <pybind11/functional.h>
 #include <pybind11/stl.h>
 
 #include "cost.h"
@@ -319,6 +320,9 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("reclaim_idle_after", [](PyPlatform& s, double now, double min_idle_s) {
         return list_json(s.p->partitions()->reclaim_idle_after(now, min_idle_s));
       }, py::call_guard<py::gil_scoped_release>())
+      .def("set_partition_actuator", [](PyPlatform& s, DiscoveryService::RemoteActuator fn) {
+        s.p->discovery()->set_remote_actuator(std::move(fn));
+      })
       .def("consolidate_partitions", [](PyPlatform& s, double now, bool plan_only) {
         return s.p->consolidate_partitions(now, !plan_only);
       }, py::arg("now"), py::arg("plan_only") = true, py::call_guard<py::gil_scoped_release>())

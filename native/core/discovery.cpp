@@ -169,10 +169,72 @@ bool DiscoveryService::gpu(const std::string& uuid, GpuDevice* out) const {
   return false;
 }
 
+namespace {
+// HAL of an agent-pushed node: discovery = the last push; actuation = the
+// remote actuator (node agent gRPC SetPartition, authenticated).
+class RemoteHal : public Hal {
+ public:
+  RemoteHal(DiscoveryService* d, std::string node) : d_(d), node_(std::move(node)) {}
+  std::string backend() const override { return "agent"; }
+  NodeTopology discover(const std::string& name) override {
+    NodeTopology n;
+    d_->pushed_node(name, &n);
+    return n;
+  }
+  void refresh_telemetry(NodeTopology&) override {}  // the agent pushes telemetry
+  std::string set_compute_partition(const std::string& gpu, ComputePartition mode) override {
+    return d_->actuate_remote(node_, gpu, to_string(mode), "");
+  }
+  std::string set_memory_partition(const std::string& gpu, MemoryPartition mode) override {
+    return d_->actuate_remote(node_, gpu, "", to_string(mode));
+  }
+
+ private:
+  DiscoveryService* d_;
+  std::string node_;
+};
+}  // namespace
+
 std::shared_ptr<Hal> DiscoveryService::hal(const std::string& node) const {
   std::lock_guard<std::mutex> lk(hal_mu_);
   auto it = hals_.find(node);
-  return it == hals_.end() ? nullptr : it->second;
+  if (it != hals_.end()) return it->second;
+  if (actuator_ && pushed_.count(node))
+    return std::make_shared<RemoteHal>(const_cast<DiscoveryService*>(this), node);
+  return nullptr;
+}
+
+void DiscoveryService::set_remote_actuator(RemoteActuator fn) {
+  std::lock_guard<std::mutex> lk(hal_mu_);
+  actuator_ = std::move(fn);
+}
+
+bool DiscoveryService::pushed_node(const std::string& name, NodeTopology* out) const {
+  std::lock_guard<std::mutex> lk(hal_mu_);
+  auto it = pushed_.find(name);
+  if (it == pushed_.end()) return false;
+  *out = it->second;
+  return true;
+}
+
+std::string DiscoveryService::actuate_remote(const std::string& node, const std::string& gpu,
+                                             const std::string& compute, const std::string& memory) {
+  RemoteActuator fn;
+  {
+    std::lock_guard<std::mutex> lk(hal_mu_);
+    fn = actuator_;
+  }
+  if (!fn) return "no remote actuator for node " + node;
+  std::string err = fn(node, gpu, compute, memory);  // no lock held across the remote call
+  if (!err.empty()) return err;
+  std::lock_guard<std::mutex> lk(hal_mu_);
+  auto it = pushed_.find(node);
+  if (it != pushed_.end())
+    if (GpuDevice* g = it->second.gpu(gpu)) {
+      if (!compute.empty()) apply_compute_partition(*g, compute_partition_from(compute));
+      if (!memory.empty()) g->partition.memory = memory_partition_from(memory);
+    }
+  return "";
 }
 
 void DiscoveryService::emit(TopologyEvent e) {

@@ -14,6 +14,7 @@
 //   * events go to a bounded ring that drops the oldest entry instead of
 //     blocking the producer; HealthChanged / LinkDown are actually emitted.
 #pragma once
+#include <functional>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -80,6 +81,17 @@ class DiscoveryService {
   bool node(const std::string& name, NodeTopology* out) const;
   bool gpu(const std::string& uuid, GpuDevice* out) const;
   std::shared_ptr<Hal> hal(const std::string& node) const;
+  // Agent-pushed nodes have no local HAL: partition switches on them go
+  // through this actuator (the controller's authenticated call to the node
+  // agent's SetPartition), and the pushed topology is updated on success.
+  // Signature: (node, gpu uuid, compute mode or "", memory mode or "") -> error.
+  using RemoteActuator = std::function<std::string(const std::string&, const std::string&,
+                                                   const std::string&, const std::string&)>;
+  void set_remote_actuator(RemoteActuator fn);
+  // Pushed-node helpers for the remote HAL.
+  bool pushed_node(const std::string& name, NodeTopology* out) const;
+  std::string actuate_remote(const std::string& node, const std::string& gpu, const std::string& compute,
+                             const std::string& memory);
 
   std::vector<TopologyHint> hints(const HintRequest& req, size_t max_results = 3) const;
 
@@ -95,6 +107,7 @@ class DiscoveryService {
   mutable std::mutex hal_mu_;
   std::map<std::string, std::shared_ptr<Hal>> hals_;
   std::map<std::string, NodeTopology> pushed_;
+  RemoteActuator actuator_;
 
   std::shared_ptr<const ClusterTopology> snap_;  // accessed with std::atomic_load/store
   std::mutex publish_mu_;                        // serialises writers only

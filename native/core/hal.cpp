@@ -112,20 +112,23 @@ std::string FakeHal::set_compute_partition(const std::string& gpu_uuid, ComputeP
   for (const auto& pi : g->partition.instances)
     if (pi.in_use) return "gpu busy: partition " + pi.id + " in use by " + pi.owner;
   if (mode == ComputePartition::TPX) return "TPX not supported on MI355X (8 XCDs)";
-  // CPX needs a memory mode whose NUMA domains divide the partitions evenly.
-  g->partition.compute = mode;
-  g->partition.instances.clear();
+  apply_compute_partition(*g, mode);
+  ++switches_;
+  return "";
+}
+
+void apply_compute_partition(GpuDevice& g, ComputePartition mode) {
+  g.partition.compute = mode;
+  g.partition.instances.clear();
   const int np = partition_count(mode);
   for (int i = 0; i < np; ++i) {
     PartitionInstance pi;
     pi.index = i;
-    pi.id = g->uuid + "/p" + std::to_string(i);
-    pi.cu_count = g->cu_count / np;
-    pi.memory_gb = g->memory_total_gb / np;
-    g->partition.instances.push_back(pi);
+    pi.id = g.uuid + "/p" + std::to_string(i);
+    pi.cu_count = g.cu_count / np;
+    pi.memory_gb = g.memory_total_gb / np;
+    g.partition.instances.push_back(pi);
   }
-  ++switches_;
-  return "";
 }
 
 std::string FakeHal::set_memory_partition(const std::string& gpu_uuid, MemoryPartition mode) {

@@ -33,6 +33,11 @@ class Hal {
                                            MemoryPartition mode) = 0;
 };
 
+// Re-slice one GPU's partition instances for a new compute mode (one slice
+// per partition, CUs and HBM split evenly) — what a successful switch does to
+// the device model, whoever actuated it.
+void apply_compute_partition(GpuDevice& g, ComputePartition mode);
+
 class FakeHal : public Hal {
  public:
   explicit FakeHal(const Json& node_fixture);

@@ -34,7 +34,7 @@ def cluster():
     for i in range(2):
         api.add_node(f"mi355x-{i}")
     cfg = load_config(DEFAULTS, sets=["listen.host=127.0.0.1", "listen.port=0", f"kube.url={api.url}",
-                                      "tickSeconds=0.2"])
+                                      "tickSeconds=0.2", "optimizer.recommendEverySeconds=0.5"])
     plat, ext, rec = build(cfg)
     from kgwe.core import make_fixture
     for i in range(2):
@@ -246,8 +246,6 @@ def test_mixed_tenancy_training_and_partition_inference(cluster):
     import yaml
     from pathlib import Path
 
-    from kgwe.optimizer.optimizer import TelemetryDataPoint, WorkloadOptimizer
-
     api, kube, plat, ext, rec = cluster
     docs = [d for d in yaml.safe_load_all((Path(__file__).parents[1] / "examples" /
                                            "mixed-tenancy.yaml").read_text()) if d]
@@ -267,15 +265,13 @@ def test_mixed_tenancy_training_and_partition_inference(cluster):
     slices = [p for a in allocs.values() for p in a["partitions"]]
     gpus = {p.rsplit("/p", 1)[0] for p in slices}
     assert len(slices) == 4 and len(gpus) == 1 and not gpus & set(train[0]["gpus"])
-    # rightsizing: low-utilisation inference telemetry -> CPX recommendation
-    opt = WorkloadOptimizer(learn=False)
-    t0 = time.time()
-    for i in range(30):
-        opt.ingest_telemetry("serve", TelemetryDataPoint(
-            timestamp=t0 + i, gpu_uuid="g0", gpu_utilization=12.0,
-            memory_used_bytes=20 * 2**30, memory_total_bytes=288 * 2**30))
-    pred = opt.predict_resources("serve", {"model_params_billions": 1, "workload_type": "Inference"})
-    assert pred.recommended_partition == "CPX"
+    # rightsizing by the RUNNING controller: the serving GPU's amd-smi telemetry
+    # (low gfx_activity) -> IngestTelemetry every tick -> status.recommendation
+    plat.fake_set_util(node["name"], next(iter(gpus)), 12.0, 20.0)
+    rec_ = wait_for(lambda: (_status(kube, "serving", "llama3-1b-serve-0").get("recommendation") or {})
+                    if (_status(kube, "serving", "llama3-1b-serve-0").get("recommendation") or {})
+                    .get("partition") == "CPX" else None, timeout=15)
+    assert rec_["gpus"] == 1
     # completion -> cost records per team; slices metered at 1/8 of a GPU
     time.sleep(0.3)
     for name, ns in [("llama3-8b-finetune", "research")] + [(f"llama3-1b-serve-{i}", "serving")
@@ -356,3 +352,129 @@ def test_not_ready_node_evicts(cluster):
                   .get("restarts") == 1 and _status(kube, "ml", "nr").get("phase") in
                   ("Scheduled", "Running") else None, timeout=15)
     assert st["scheduledNode"] != first and "NotReady" in st["lastFailure"]
+
+
+def _cluster(sets: list[str], nodes: int = 2):
+    api = FakeApiServer().start()
+    kube = KubeClient(api.url)
+    for i in range(nodes):
+        api.add_node(f"mi355x-{i}")
+    cfg = load_config(DEFAULTS, sets=["listen.host=127.0.0.1", "listen.port=0", f"kube.url={api.url}",
+                                      "tickSeconds=0.2"] + sets)
+    plat, ext, rec = build(cfg)
+    from kgwe.core import make_fixture
+    for i in range(nodes):
+        plat.add_fake_node(make_fixture(f"mi355x-{i}", 8, 2))
+    ext.start()
+    rec.start()
+    sim = SchedulerSim(kube, ext.url).start()
+
+    def stop():
+        sim.stop()
+        rec.stop()
+        ext.stop()
+        api.stop()
+    return api, kube, plat, ext, rec, stop
+
+
+def test_optimizer_loop_recommends_cpx_from_live_telemetry():
+    """The running controller feeds per-allocation telemetry to the optimizer,
+    writes status.recommendation (rightsizing) and trains the online model on
+    completions — no hand-fed optimizer object."""
+    api, kube, plat, ext, rec, stop = _cluster(["optimizer.recommendEverySeconds=0.5"])
+    try:
+        kube.create_cr(gw("serve", count=0, workloadType="Inference", framework="PyTorch",
+                          gpuRequirements={"count": 0, "partition": {"mode": "CPX", "count": 1}},
+                          distributedConfig={"backend": "RCCL"}))
+        kube.create_cr(gw("train", count=2))
+        st = wait_for(lambda: _status(kube, "ml", "serve") if _status(kube, "ml", "serve")
+                      .get("phase") in ("Scheduled", "Running") else None, timeout=10)
+        assert "recommendation" in st  # PredictResources at admission
+        gpu = st["partitionSlices"][0].rsplit("/p", 1)[0]
+        plat.fake_set_util(st["scheduledNode"], gpu, 12.0, 20.0)  # a lightly loaded server
+        tr = wait_for(lambda: _status(kube, "ml", "train") if _status(kube, "ml", "train")
+                      .get("phase") in ("Scheduled", "Running") else None, timeout=10)
+        for g in tr["allocatedGPUs"]:
+            plat.fake_set_util(tr["scheduledNode"], g, 97.0, 200.0)
+        r = wait_for(lambda: (_status(kube, "ml", "serve").get("recommendation") or {})
+                     if (_status(kube, "ml", "serve").get("recommendation") or {}).get("partition") == "CPX"
+                     else None, timeout=15)
+        assert r["gpus"] == 1 and r["expectedUtilization"] < 40
+        rt = _status(kube, "ml", "train").get("recommendation") or {}
+        assert rt.get("partition") is None  # a busy training job is not squeezed into a slice
+        m = rec.optimizer.GetMetrics()
+        assert m["total_samples"] >= 20 and {"ml/serve", "ml/train"} <= set(m["profiles"])
+        # completion -> a training row of the online model
+        kube.patch_pod("ml", "serve-gw", {"status": {"phase": "Succeeded"}})
+        wait_for(lambda: (rec.optimizer.GetMetrics().get("model") or {}).get("training_rows", 0) > 0,
+                 timeout=10)
+        assert rec.errors == 0
+    finally:
+        stop()
+
+
+def test_controller_consolidates_partitions_by_eviction():
+    """Under-used CPX GPUs are emptied by evicting their preemptible inference
+    pods (re-created and packed onto the fuller GPU), then go back to SPX."""
+    api, kube, plat, ext, rec, stop = _cluster(["partitionConsolidateAfterSeconds=0",
+                                                "partitionReclaimIdleSeconds=3600"], nodes=1)
+    try:
+        for i in range(12):
+            kube.create_cr(gw(f"inf-{i}", count=0, workloadType="Inference",
+                              gpuRequirements={"count": 0, "partition": {"mode": "CPX", "count": 1}},
+                              distributedConfig={"backend": "RCCL"}))
+        wait_for(lambda: plat.scheduler_metrics()["allocated_partitions"] == 12, timeout=20)
+        assert plat.partition_metrics()["modes"]["CPX"]["gpus"] == 2
+        # finish most pods on the first (full) GPU: it drops under the threshold
+        by_gpu = {}
+        for a in plat.allocations():
+            by_gpu.setdefault(a["partitions"][0].rsplit("/p", 1)[0], []).append(a["uid"])
+        full = max(by_gpu.values(), key=len)
+        pods = {p["metadata"]["uid"]: p["metadata"]["name"] for p in kube.list_pods("ml")}
+        for uid in full[:6]:
+            kube.patch_pod("ml", pods[uid], {"status": {"phase": "Succeeded"}})
+        wait_for(lambda: plat.partition_metrics()["modes"].get("CPX", {}).get("gpus") == 1
+                 and plat.scheduler_metrics()["allocated_partitions"] == 6, timeout=20)
+        m = plat.partition_metrics()
+        assert m["slice_utilization"] == pytest.approx(6 / 8)
+        moved = [n for n in (f"inf-{i}" for i in range(12)) if _status(kube, "ml", n).get("migrations")]
+        assert moved and rec.migrations == len(moved)
+        assert all(_status(kube, "ml", n)["phase"] in ("Scheduled", "Running") for n in moved)
+        assert rec.errors == 0
+    finally:
+        stop()
+
+
+def test_failover_keeps_scheduling_semantics_and_cost(tmp_path):
+    """A new leader restores the FULL ledger entry (priority, preemptible, type,
+    gang) and resumes the running cost record from the journal: a
+    non-preemptible job survives a high-priority arrival after failover and
+    is metered for its whole run."""
+    journal = tmp_path / "cost.jsonl"
+    sets = [f"cost.journalPath={journal}"]
+    api, kube, plat, ext, rec, stop = _cluster(sets, nodes=1)
+    try:
+        kube.create_cr(gw("keep", count=8, priority=10, preemptible=False))
+        wait_for(lambda: plat.scheduler_metrics()["allocated_gpus"] == 8)
+        t_bind = time.time()
+        time.sleep(1.2)
+        plat.tick(time.time())  # a metering sample -> journal checkpoint path
+        rec.stop()  # leader lost
+        cfg = load_config(DEFAULTS, sets=["listen.host=127.0.0.1", "listen.port=0", f"kube.url={api.url}"]
+                          + sets)
+        plat2, ext2, rec2 = build(cfg)
+        from kgwe.core import make_fixture
+        plat2.add_fake_node(make_fixture("mi355x-0", 8, 2))
+        assert rec2.rebuild_ledger() == 1
+        assert plat2.cost_resumed() == 1
+        a = plat2.allocations()[0]
+        assert a["preemptible"] is False and a["priority"] == 10 and a["type"] == "Training"
+        d = plat2.schedule({"uid": "vip", "priority": 1000, "gpuRequirements": {"count": 8}})
+        assert not d["ok"] and "keep" not in str(d.get("preempted"))
+        time.sleep(0.3)
+        rel = plat2.release(a["uid"])
+        dur = rel["cost"]["duration_s"]
+        assert dur >= time.time() - t_bind - 0.5  # metered from the first leader's bind
+        ext2.httpd.server_close()
+    finally:
+        stop()
