@@ -1,14 +1,21 @@
 """kube-scheduler stand-in that drives the extender over HTTP.
 
 Runs the scheduling cycle kube-scheduler runs for a second-scheduler profile
-(``schedulerName: kgwe-scheduler``, reference scheduler-configmap.yaml:18-60)
-with the extender configured ``nodeCacheCapable: false`` (full Node objects in
-ExtenderArgs): watch unscheduled pods -> POST /filter -> POST /prioritize ->
-pick the highest score -> POST /bind.  Used by tests and by the latency
-benchmark where no real kube-scheduler exists.
+(``schedulerName: kgwe-scheduler``, reference scheduler-configmap.yaml:18-60):
+watch unscheduled pods -> POST /filter -> POST /prioritize -> pick the highest
+score -> POST /bind.  ``node_cache_capable=False`` (the reference's setting)
+sends full Node objects in every ExtenderArgs, True sends node names only.
+When no node passes and the pod has a priority, it runs kube-scheduler's
+PostFilter with the extender's ``preempt`` verb: the extender names the
+victims per node, the stand-in evicts the cheapest node's victims (deletes
+the pods) and retries the preemptor.  Used by tests and by the latency
+benchmark where no real kube-scheduler exists.  Node objects are serialised
+once per node-list refresh (kube-scheduler keeps them encoded in its cache
+too), so the stand-in's own cost stays out of the measured latency.
 """
 from __future__ import annotations
 
+import gc
 import http.client
 import json
 import queue
@@ -27,8 +34,8 @@ class _Http:
         self.host, self.port, self.prefix = u.hostname, u.port, u.path.rstrip("/")
         self.local = threading.local()
 
-    def post(self, verb: str, obj) -> object:
-        data = json.dumps(obj).encode()
+    def post(self, verb: str, obj, raw: bool = False) -> object:
+        data = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj).encode()
         for attempt in range(2):
             c = getattr(self.local, "c", None)
             if c is None:
@@ -37,7 +44,8 @@ class _Http:
                 c.request("POST", f"{self.prefix}/{verb}", body=data,
                           headers={"Content-Type": "application/json"})
                 r = c.getresponse()
-                return json.loads(r.read() or b"null")
+                body = r.read() or b"null"
+                return body if raw else json.loads(body)
             except (http.client.HTTPException, OSError):
                 self.local.c = None
                 if attempt:
@@ -52,41 +60,151 @@ def _ready(node: dict) -> bool:
 
 class SchedulerSim:
     def __init__(self, kube: KubeClient, extender_url: str, bind_workers: int = 4,
-                 on_bound=None, on_failed=None, retry_interval_s: float = 0.05):
+                 on_bound=None, on_failed=None, retry_interval_s: float = 0.05,
+                 node_cache_capable: bool = False, preempt: bool = True, on_preempted=None,
+                 node_refresh_s: float = 1.0, adaptive_nodes_to_score: bool = True):
         self.kube = kube
         self.ext = _Http(extender_url)
         self.on_bound = on_bound
         self.on_failed = on_failed
+        self.on_preempted = on_preempted
         self.retry = retry_interval_s
+        self.node_cache_capable = node_cache_capable
+        self.node_refresh_s = node_refresh_s  # unused: the node cache follows a watch (see _informer)
+        self.adaptive = adaptive_nodes_to_score
+        self._start = 0  # kube-scheduler's rotating start index over the node list
+        self.preempt = preempt
+        self._node_json: dict[str, bytes] = {}
+        self._node_rv: dict[str, str] = {}
+        self._objs: dict = {}
+        self._list_rv = None
+        self._bound: dict[str, tuple] = {}  # pod uid -> (namespace, name) of bound pods
+        self.retried: set = set()            # uids of pods that needed more than one cycle
+        self._attempts: dict[str, int] = {}
         self._q: queue.Queue = queue.Queue()
         self._bind_q: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._nodes: list = []
         self._nodes_at = 0.0
+        self._nodes_lock = threading.Lock()
         self._threads = [threading.Thread(target=self._watch, daemon=True),
-                         threading.Thread(target=self._cycle, daemon=True)]
+                         threading.Thread(target=self._cycle, daemon=True),
+                         threading.Thread(target=self._informer, daemon=True)]
         self._threads += [threading.Thread(target=self._binder, daemon=True)
                           for _ in range(bind_workers)]
-        self.stats = {"scheduled": 0, "unschedulable": 0, "bind_errors": 0}
+        self._rt = {"filter": [], "prioritize": [], "cycle": []}  # client-side round trips (s)
+        self.stats = {"scheduled": 0, "unschedulable": 0, "bind_errors": 0, "preemptions": 0,
+                      "preempt_calls": 0}
 
     def start(self) -> "SchedulerSim":
+        try:  # WaitForCacheSync: the node cache is warm before the first cycle
+            self._refresh_nodes()
+        except Exception:  # noqa: BLE001
+            pass
+        # The cached fleet is long-lived: keep it out of CPython's cyclic GC,
+        # whose full collections over ~10^6 Node-object dicts paused every
+        # thread of the stand-in for ~100 ms (kube-scheduler has no such pause).
+        gc.freeze()
         for t in self._threads:
             t.start()
         return self
 
     def stop(self) -> None:
         self._stop.set()
+        for k, v in self._rt.items():  # client-observed round trips, ms
+            if v:
+                v = sorted(v)
+                self.stats[f"{k}_rt_ms"] = {"p50": round(1000 * v[len(v) // 2], 3),
+                                            "p99": round(1000 * v[min(len(v) - 1, int(len(v) * 0.99))], 3),
+                                            "mean": round(1000 * sum(v) / len(v), 3)}
+
+    def _refresh_nodes(self) -> None:
+        """Full re-list (start-up, invalidate_nodes, watch failure)."""
+        res = self.kube.request("GET", "/api/v1/nodes")
+        objs = {n["metadata"]["name"]: n for n in res.get("items", [])}
+        self._set_nodes(objs, str((res.get("metadata") or {}).get("resourceVersion", "0")))
+
+    def _set_nodes(self, objs: dict, rv: str) -> None:
+        # kube-scheduler never offers a node that is not Ready (the
+        # node.kubernetes.io/not-ready taint): neither does the stand-in.
+        # Re-serialise only nodes whose resourceVersion moved.
+        old, old_rv = self._node_json, self._node_rv
+        node_json, node_rv, nodes = {}, {}, []
+        for name, n in objs.items():
+            if not _ready(n):
+                continue
+            nodes.append(n)
+            v = n["metadata"].get("resourceVersion")
+            node_rv[name] = v
+            node_json[name] = old[name] if v is not None and old_rv.get(name) == v and name in old \
+                else json.dumps(n).encode()
+        with self._nodes_lock:  # swap all at once: a cycle never sees a half-built cache
+            self._objs, self._list_rv = objs, rv
+            self._nodes, self._node_json, self._node_rv = nodes, node_json, node_rv
+            self._nodes_at = time.time()
+
+    def _informer(self):
+        """kube-scheduler's node informer: list once, then apply watch events
+        off the scheduling cycle.  (Re-listing 1,250 full Node objects parses
+        ~9 MB under the GIL — ~0.2 s that stalled every pod queued behind it.)"""
+        while not self._stop.is_set():
+            with self._nodes_lock:
+                rv, objs = self._list_rv, self._objs
+            if rv is None:
+                self._stop.wait(0.05)
+                continue
+            try:
+                evs, new_rv = self.kube.watch("/api/v1/nodes", rv, timeout_s=1)
+            except Exception:  # noqa: BLE001
+                self._stop.wait(0.2)
+                try:
+                    self._refresh_nodes()
+                except Exception:  # noqa: BLE001
+                    pass
+                continue
+            if not evs:
+                with self._nodes_lock:
+                    if self._list_rv == rv:
+                        self._list_rv = new_rv
+                continue
+            objs = dict(objs)
+            for e in evs:
+                o = e.get("object") or {}
+                name = (o.get("metadata") or {}).get("name")
+                if not name:
+                    continue
+                if e.get("type") == "DELETED":
+                    objs.pop(name, None)
+                else:
+                    objs[name] = o
+            self._set_nodes(objs, new_rv)
 
     def _nodelist(self) -> list:
-        if time.time() - self._nodes_at > 1.0 or not self._nodes:
-            # kube-scheduler never offers a node that is not Ready (the
-            # node.kubernetes.io/not-ready taint): neither does the stand-in.
-            self._nodes = [n for n in self.kube.list_nodes() if _ready(n)]
-            self._nodes_at = time.time()
-        return self._nodes
+        if not self._nodes:
+            self._refresh_nodes()
+        with self._nodes_lock:
+            return self._nodes
+
+    def _args(self, pod_json: bytes, names: list) -> bytes:
+        if self.node_cache_capable:
+            return b'{"pod":' + pod_json + b',"nodenames":' + json.dumps(names).encode() + b"}"
+        with self._nodes_lock:
+            nj = self._node_json
+        return (b'{"pod":' + pod_json + b',"nodes":{"items":[' +
+                b",".join(nj[n] for n in names if n in nj) + b"]}}")
+
+    def _passed(self, reply: bytes) -> list:
+        from ..core import native  # noqa: PLC0415
+
+        try:
+            return native.scan_node_names(reply)  # C++ scanner: names of the returned items
+        except Exception:  # noqa: BLE001
+            d = json.loads(reply or b"{}")
+            return [n["metadata"]["name"] for n in (d.get("nodes") or {}).get("items", [])] + \
+                list(d.get("nodenames") or [])
 
     def invalidate_nodes(self) -> None:
-        self._nodes_at = 0.0
+        self._refresh_nodes()
 
     def _watch(self):
         rv = "0"
@@ -109,28 +227,87 @@ class SchedulerSim:
                 pod, seen = self._q.get(timeout=0.2)
             except queue.Empty:
                 continue
+            t_cycle = time.perf_counter()
+            pod.setdefault("_kgwe_t", {})["seen"] = seen
+            pod["_kgwe_t"]["cycle"] = t_cycle
             nodes = self._nodelist()
+            names = self._candidates([n["metadata"]["name"] for n in nodes])
+            pod_json = json.dumps({k: v for k, v in pod.items() if k != "_kgwe_t"}).encode()
             try:
-                fr = self.ext.post("filter", {"pod": pod, "nodes": {"items": nodes}})
+                t_f = time.perf_counter()
+                passed = self._passed(self.ext.post("filter", self._args(pod_json, names), raw=True))
+                self._rt["filter"].append(time.perf_counter() - t_f)
             except Exception:  # noqa: BLE001
                 self._requeue(pod, seen)
                 continue
-            passed = [n for n in (fr or {}).get("nodes", {}).get("items", [])]
             if not passed:
                 self.stats["unschedulable"] += 1
                 if self.on_failed:
-                    self.on_failed(pod, fr)
+                    self.on_failed(pod, None)
+                if self.preempt and int((pod.get("spec") or {}).get("priority") or 0) > 0:
+                    self._post_filter(pod, names)
                 self._requeue(pod, seen)
                 continue
-            pr = self.ext.post("prioritize", {"pod": pod, "nodes": {"items": passed}}) or []
+            t_p = time.perf_counter()
+            pr = self.ext.post("prioritize", self._args(pod_json, passed)) or []
+            self._rt["prioritize"].append(time.perf_counter() - t_p)
             scores = {h["host"]: h["score"] for h in pr}
-            best = max((n["metadata"]["name"] for n in passed),
-                       key=lambda nm: (scores.get(nm, 0), -hash(nm) % 1000, nm))
+            best = max(passed, key=lambda nm: (scores.get(nm, 0), -hash(nm) % 1000, nm))
+            pod["_kgwe_t"]["bind_q"] = time.perf_counter()
             self._bind_q.put((pod, best, seen))
+            self._rt["cycle"].append(time.perf_counter() - t_cycle)
+
+    def _candidates(self, names: list) -> list:
+        """kube-scheduler's percentageOfNodesToScore (adaptive default): it
+        stops searching after max(100, N * max(5, 50 - N / 125) %) feasible
+        nodes, starting where the previous cycle stopped, and only those reach
+        the extender.  (Its own plugins would also drop full nodes; the
+        extender filter covers that here.)"""
+        n = len(names)
+        if not self.adaptive or n <= 100:
+            return names
+        pct = max(5.0, 50.0 - n / 125.0)
+        k = min(n, max(100, int(n * pct / 100.0)))
+        start = self._start % n
+        self._start = start + k
+        return (names + names)[start:start + k]
+
+    def _post_filter(self, pod: dict, names: list) -> None:
+        """kube-scheduler PostFilter (DefaultPreemption) through the extender's
+        preempt verb: pick the node needing the fewest evictions, evict them."""
+        self.stats["preempt_calls"] += 1
+        try:
+            res = self.ext.post("preempt", {"pod": pod, "nodeNameToMetaVictims": {
+                n: {"pods": [], "numPDBViolations": 0} for n in names}}) or {}
+        except Exception:  # noqa: BLE001
+            return
+        plans = {n: [p["uid"] for p in (v or {}).get("pods") or []]
+                 for n, v in (res.get("nodeNameToMetaVictims") or {}).items()}
+        plans = {n: v for n, v in plans.items() if v}
+        if not plans:
+            return
+        node = min(plans, key=lambda n: (len(plans[n]), n))
+        victims = plans[node]
+        for uid in victims:
+            ref = self._bound.pop(uid, None)
+            if ref is not None:
+                try:
+                    self.kube.delete_pod(ref[0], ref[1])
+                except Exception:  # noqa: BLE001
+                    pass
+        self.stats["preemptions"] += len(victims)
+        if self.on_preempted:
+            self.on_preempted(victims)
 
     def _requeue(self, pod, seen):
+        uid = pod["metadata"].get("uid", "")
+        self.retried.add(uid)
+        # kube-scheduler backoff: doubling from the retry interval, capped at 1 s
+        n = self._attempts[uid] = self._attempts.get(uid, 0) + 1
+        delay = min(1.0, self.retry * (2 ** min(n - 1, 6)))
+
         def later():
-            time.sleep(self.retry)
+            time.sleep(delay)
             if not self._stop.is_set():
                 self._q.put((pod, seen))
         threading.Thread(target=later, daemon=True).start()
@@ -142,6 +319,7 @@ class SchedulerSim:
             except queue.Empty:
                 continue
             md = pod["metadata"]
+            pod.setdefault("_kgwe_t", {})["bind"] = time.perf_counter()
             try:
                 res = self.ext.post("bind", {"podName": md["name"], "podNamespace": md.get("namespace", "default"),
                                              "podUID": md.get("uid", ""), "node": node}) or {}
@@ -155,6 +333,7 @@ class SchedulerSim:
                     self._requeue(pod, seen)
                 continue
             self.stats["scheduled"] += 1
+            self._bound[md.get("uid", "")] = (md.get("namespace", "default"), md["name"])
             if self.on_bound:
                 self.on_bound(pod, node, time.perf_counter())
 

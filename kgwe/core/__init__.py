@@ -110,6 +110,21 @@ class Platform:
     def prioritize(self, body: str) -> str:
         return self._p.prioritize(body)
 
+    def preempt(self, body: str) -> str:
+        """ExtenderPreemptionArgs -> ExtenderPreemptionResult."""
+        return self._p.preempt(body)
+
+    def count_preemptions(self, n: int) -> None:
+        """Victims actually evicted after a preempt verb (kgwe_preemptions_total)."""
+        self._p.count_preemptions(n)
+
+    def filter_bytes(self, body: bytes) -> bytes:
+        """filter() without UTF-8 decode/encode of the (multi-MB) bodies."""
+        return self._p.filter_bytes(body)
+
+    def prioritize_bytes(self, body: bytes) -> bytes:
+        return self._p.prioritize_bytes(body)
+
     def bind(self, body: str, pod: dict | None = None) -> dict:
         return _j(self._p.bind(body, json.dumps(pod) if pod else ""))
 

@@ -109,8 +109,19 @@ class ExtenderServer:
 
             def do_POST(self):
                 n = int(self.headers.get("Content-Length") or 0)
-                body = self.rfile.read(n).decode() if n else "{}"
+                raw = self.rfile.read(n) if n else b"{}"
                 path = self.path.split("?")[0]
+                verb = path[len(outer.prefix):].strip("/")
+                if verb in ("filter", "prioritize") and not outer.tracer.exporter:
+                    # hot path: bytes straight into the C++ scanner and back
+                    try:
+                        with outer.tracer.phase(verb, None, verb=verb):
+                            data = (outer.platform.filter_bytes(raw) if verb == "filter"
+                                    else outer.platform.prioritize_bytes(raw))
+                    except Exception as e:  # noqa: BLE001 - contract: errors go in the body
+                        data = json.dumps({"error": f"{type(e).__name__}: {e}"}).encode()
+                    return self._send(200, data)
+                body = raw.decode()
                 for pre, fn in outer.routes.items():
                     if path.startswith(pre):
                         try:
@@ -130,6 +141,9 @@ class ExtenderServer:
                     elif verb == "bind":
                         with outer.tracer.phase("bind", key, verb="bind"):
                             out = json.dumps(outer.handle_bind(body))
+                    elif verb == "preempt":
+                        with outer.tracer.phase("preempt", key, verb="preempt"):
+                            out = outer.platform.preempt(body)
                     else:
                         return self._send(404, b'{"error":"unknown verb"}')
                 except Exception as e:  # noqa: BLE001 - contract: errors go in the body

@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "cost.h"
+#include "extender_scan.h"
 #include "hal.h"
 #include "histogram.h"
 #include "platform.h"
@@ -130,6 +131,11 @@ PYBIND11_MODULE(_kgwe_core, m) {
     return to_json(workload_from_json(Json::parse(wl))).dump();
   });
   m.def("json_roundtrip", [](const std::string& s) { return Json::parse(s).dump(); });
+  m.def("scan_node_names", [](const std::string& s) {
+    std::vector<std::string> names;
+    if (!scan_node_names(s, &names)) throw std::runtime_error("not an ExtenderArgs / FilterResult document");
+    return names;
+  }, py::call_guard<py::gil_scoped_release>());
 
   py::class_<LatencyHistogram>(m, "LatencyHistogram")
       .def(py::init<>())
@@ -154,29 +160,29 @@ PYBIND11_MODULE(_kgwe_core, m) {
         }
         s.p->discovery()->add_node(name, hal);
         return name;
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("add_amdsmi_node", [](PyPlatform& s, const std::string& name) {
         auto hal = std::make_shared<AmdSmiHal>();
         if (!hal->ok()) throw std::runtime_error("amd-smi unavailable: " + hal->error());
         s.p->discovery()->add_node(name, hal);
         return name;
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("upsert_node", [](PyPlatform& s, const std::string& node_json) {
         s.p->discovery()->upsert_node(node_from_json(Json::parse(node_json)));
-      })
-      .def("remove_node", [](PyPlatform& s, const std::string& n) { s.p->discovery()->remove_node(n); })
-      .def("set_cordon", [](PyPlatform& s, const std::string& n, bool on) { s.p->scheduler()->set_cordon(n, on); })
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("remove_node", [](PyPlatform& s, const std::string& n) { s.p->discovery()->remove_node(n); }, py::call_guard<py::gil_scoped_release>())
+      .def("set_cordon", [](PyPlatform& s, const std::string& n, bool on) { s.p->scheduler()->set_cordon(n, on); }, py::call_guard<py::gil_scoped_release>())
       .def("cordoned", [](PyPlatform& s) { return s.p->scheduler()->cordoned(); })
       .def("refresh", [](PyPlatform& s) { s.p->discovery()->refresh(); },
            py::call_guard<py::gil_scoped_release>())
       .def("refresh_telemetry", [](PyPlatform& s) { s.p->discovery()->refresh_telemetry(); },
            py::call_guard<py::gil_scoped_release>())
-      .def("snapshot_json", [](PyPlatform& s) { return to_json(*s.p->discovery()->snapshot()).dump(); })
+      .def("snapshot_json", [](PyPlatform& s) { return to_json(*s.p->discovery()->snapshot()).dump(); }, py::call_guard<py::gil_scoped_release>())
       .def("node_json", [](PyPlatform& s, const std::string& n) {
         NodeTopology t;
         if (!s.p->discovery()->node(n, &t)) return std::string("null");
         return to_json(t).dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("generation", [](PyPlatform& s) { return s.p->discovery()->generation(); })
       .def("topology_events_json", [](PyPlatform& s) {
         Json a = Json::array();
@@ -189,7 +195,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
           a.push_back(j);
         }
         return a.dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("hints_json", [](PyPlatform& s, int count, double min_mem, const std::string& arch) {
         HintRequest r;
         r.gpu_count = count;
@@ -210,39 +216,65 @@ PYBIND11_MODULE(_kgwe_core, m) {
           a.push_back(j);
         }
         return a.dump();
-      }, py::arg("count"), py::arg("min_memory_gb") = 0.0, py::arg("arch") = "")
+      }, py::arg("count"), py::arg("min_memory_gb") = 0.0, py::arg("arch") = "", py::call_guard<py::gil_scoped_release>())
       // ---- fault injection on fake nodes
       .def("fake_set_link_up", [](PyPlatform& s, const std::string& node, const std::string& a,
                                   const std::string& b, bool up) {
         s.fake(node).set_link_up(a, b, up);
         s.p->discovery()->refresh_node(node);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("fake_set_health", [](PyPlatform& s, const std::string& node, const std::string& gpu,
                                  const std::string& status, const std::string& reason) {
         s.fake(node).set_health(gpu, health_from(status), reason);
         s.p->discovery()->refresh_node(node);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("fake_set_health_signals", [](PyPlatform& s, const std::string& node, const std::string& gpu,
                                          const std::string& js) {
         s.fake(node).set_health_signals(gpu, Json::parse(js));
         s.p->discovery()->refresh_node(node);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("fake_set_util", [](PyPlatform& s, const std::string& node, const std::string& gpu,
                                double gfx, double mem_gb) {
         s.fake(node).set_util(gpu, gfx, mem_gb);
         s.p->discovery()->refresh_node(node);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("fake_set_measured_link", [](PyPlatform& s, const std::string& node, const std::string& a,
                                         const std::string& b, double gbps) {
         s.fake(node).set_measured_link(a, b, gbps);
         s.p->discovery()->refresh_node(node);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("fake_partition_switches", [](PyPlatform& s, const std::string& node) {
         return s.fake(node).partition_switches();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       // ---- extender verbs
       .def("filter", [](PyPlatform& s, const std::string& b) { return s.p->filter(b); },
            py::call_guard<py::gil_scoped_release>())
+      // bytes in / bytes out (the HTTP shell: no UTF-8 decode / encode of
+      // multi-megabyte ExtenderArgs with full Node objects)
+      .def("filter_bytes", [](PyPlatform& s, const py::bytes& b) {
+        std::string in = b;
+        std::string out;
+        {
+          py::gil_scoped_release nogil;
+          out = s.p->filter(in);
+        }
+        return py::bytes(out);
+      })
+      .def("prioritize_bytes", [](PyPlatform& s, const py::bytes& b) {
+        std::string in = b;
+        std::string out;
+        {
+          py::gil_scoped_release nogil;
+          out = s.p->prioritize(in);
+        }
+        return py::bytes(out);
+      })
+      .def("preempt", [](PyPlatform& s, const std::string& b) { return s.p->preempt(b); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("count_preemptions", [](PyPlatform& s, size_t n) {
+        s.p->scheduler()->count_preemptions(n);
+        s.p->metrics()->add("kgwe_preemptions_total", {}, static_cast<double>(n));
+      })
       .def("prioritize", [](PyPlatform& s, const std::string& b) { return s.p->prioritize(b); },
            py::call_guard<py::gil_scoped_release>())
       .def("bind", [](PyPlatform& s, const std::string& b, const std::string& pod) { return s.p->bind(b, pod); },
@@ -257,13 +289,13 @@ PYBIND11_MODULE(_kgwe_core, m) {
         for (const auto& j : parsed.items()) ws.push_back(workload_from_json(j));
         return list_json(s.p->scheduler()->schedule_gang(ws));
       }, py::call_guard<py::gil_scoped_release>())
-      .def("release", [](PyPlatform& s, const std::string& uid, double now) { return s.p->release(uid, now); })
-      .def("permit", [](PyPlatform& s, const std::string& uid) { return s.p->scheduler()->permit(uid); })
+      .def("release", [](PyPlatform& s, const std::string& uid, double now) { return s.p->release(uid, now); }, py::call_guard<py::gil_scoped_release>())
+      .def("permit", [](PyPlatform& s, const std::string& uid) { return s.p->scheduler()->permit(uid); }, py::call_guard<py::gil_scoped_release>())
       .def("restore_allocation", [](PyPlatform& s, const std::string& js) {
         return s.p->scheduler()->restore(allocation_from_json(Json::parse(js)));
-      })
-      .def("allocations_json", [](PyPlatform& s) { return list_json(s.p->scheduler()->allocations()); })
-      .def("scheduler_metrics_json", [](PyPlatform& s) { return metrics_json(s.p->scheduler()->metrics()).dump(); })
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("allocations_json", [](PyPlatform& s) { return list_json(s.p->scheduler()->allocations()); }, py::call_guard<py::gil_scoped_release>())
+      .def("scheduler_metrics_json", [](PyPlatform& s) { return metrics_json(s.p->scheduler()->metrics()).dump(); }, py::call_guard<py::gil_scoped_release>())
       .def("latency_quantile_ms", [](PyPlatform& s, double q) { return s.p->scheduler()->latency().quantile_ms(q); })
       .def("scheduler_events_json", [](PyPlatform& s) {
         Json a = Json::array();
@@ -276,7 +308,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
           a.push_back(j);
         }
         return a.dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("score_node_json", [](PyPlatform& s, const std::string& node, const std::string& w) {
         NodeTopology n;
         if (!s.p->discovery()->node(node, &n)) return std::string("null");
@@ -299,24 +331,24 @@ PYBIND11_MODULE(_kgwe_core, m) {
         for (const auto& x : sc.partitions) p.push_back(x);
         j["partitions"] = p;
         return j.dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       // ---- partitions
       .def("register_strategy", [](PyPlatform& s, const std::string& js) {
         return s.p->partitions()->register_strategy(strategy_from_json(Json::parse(js)));
-      })
-      .def("strategies_json", [](PyPlatform& s) { return list_json(s.p->partitions()->strategies()); })
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("strategies_json", [](PyPlatform& s) { return list_json(s.p->partitions()->strategies()); }, py::call_guard<py::gil_scoped_release>())
       .def("ensure_partitions", [](PyPlatform& s, const std::string& mode, int count, bool plan_only,
                                    const std::string& memory) {
         MemoryPartition m = memory_partition_from(memory.empty() ? "NPS1" : memory);
         return list_json(s.p->partitions()->ensure_capacity(compute_partition_from(mode), count, plan_only,
                                                             memory.empty() ? nullptr : &m));
-      }, py::arg("mode"), py::arg("count"), py::arg("plan_only") = false, py::arg("memory") = "")
+      }, py::arg("mode"), py::arg("count"), py::arg("plan_only") = false, py::arg("memory") = "", py::call_guard<py::gil_scoped_release>())
       .def("rebalance", [](PyPlatform& s, const std::string& name, bool plan_only) {
         return list_json(s.p->partitions()->rebalance(name, plan_only));
-      }, py::arg("name"), py::arg("plan_only") = false)
+      }, py::arg("name"), py::arg("plan_only") = false, py::call_guard<py::gil_scoped_release>())
       .def("reclaim_idle_partitions", [](PyPlatform& s, bool plan_only) {
         return list_json(s.p->partitions()->reclaim_idle(plan_only));
-      }, py::arg("plan_only") = false)
+      }, py::arg("plan_only") = false, py::call_guard<py::gil_scoped_release>())
       .def("reclaim_idle_after", [](PyPlatform& s, double now, double min_idle_s) {
         return list_json(s.p->partitions()->reclaim_idle_after(now, min_idle_s));
       }, py::call_guard<py::gil_scoped_release>())
@@ -332,7 +364,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("count_error", [](PyPlatform& s, const std::string& step) {
         s.p->metrics()->add("kgwe_controller_errors_total", {step}, 1.0);
       })
-      .def("partition_ops_json", [](PyPlatform& s) { return list_json(s.p->partitions()->operations()); })
+      .def("partition_ops_json", [](PyPlatform& s) { return list_json(s.p->partitions()->operations()); }, py::call_guard<py::gil_scoped_release>())
       .def("partition_metrics_json", [](PyPlatform& s) {
         PartitionMetrics pm = s.p->partitions()->metrics();
         Json j = Json::object();
@@ -351,7 +383,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
         j["ops_pending"] = pm.ops_pending;
         j["migrations"] = s.p->partitions()->migrations();
         return j.dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       // ---- sharing
       .def("share_allocate", [](PyPlatform& s, const std::string& js) {
         Json j = Json::parse(js);
@@ -373,41 +405,41 @@ PYBIND11_MODULE(_kgwe_core, m) {
         Json out = to_json(a);
         out["error"] = err;
         return out.dump();
-      })
-      .def("share_release", [](PyPlatform& s, const std::string& uid) { return s.p->sharing()->release(uid); })
-      .def("share_allocations_json", [](PyPlatform& s) { return list_json(s.p->sharing()->allocations()); })
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("share_release", [](PyPlatform& s, const std::string& uid) { return s.p->sharing()->release(uid); }, py::call_guard<py::gil_scoped_release>())
+      .def("share_allocations_json", [](PyPlatform& s) { return list_json(s.p->sharing()->allocations()); }, py::call_guard<py::gil_scoped_release>())
       // ---- cost
       .def("cost_start", [](PyPlatform& s, const std::string& js, double now) {
         return s.p->cost()->start(usage_from_json(Json::parse(js)), now);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("cost_sample", [](PyPlatform& s, const std::string& uid, double gfx, double mem, double now) {
         return s.p->cost()->sample(uid, gfx, mem, now);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("cost_finalize", [](PyPlatform& s, const std::string& uid, double now) {
         UsageRecord r;
         if (!s.p->cost()->finalize(uid, now, &r)) return std::string("null");
         return to_json(r).dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("cost_record_json", [](PyPlatform& s, const std::string& uid) {
         UsageRecord r;
         if (!s.p->cost()->record(uid, &r)) return std::string("null");
         return to_json(r).dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("create_budget", [](PyPlatform& s, const std::string& js, double now) {
         return s.p->cost()->create_budget(budget_from_json(Json::parse(js)), now);
-      })
-      .def("budgets_json", [](PyPlatform& s, double now) { return list_json(s.p->cost()->budgets(now)); })
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("budgets_json", [](PyPlatform& s, double now) { return list_json(s.p->cost()->budgets(now)); }, py::call_guard<py::gil_scoped_release>())
       .def("alerts_json", [](PyPlatform& s, bool unack) { return list_json(s.p->cost()->alerts(unack)); },
-           py::arg("unacknowledged_only") = false)
-      .def("acknowledge_alert", [](PyPlatform& s, const std::string& id) { return s.p->cost()->acknowledge(id); })
+           py::arg("unacknowledged_only") = false, py::call_guard<py::gil_scoped_release>())
+      .def("acknowledge_alert", [](PyPlatform& s, const std::string& id) { return s.p->cost()->acknowledge(id); }, py::call_guard<py::gil_scoped_release>())
       .def("cost_summary_json", [](PyPlatform& s, const std::string& scope, const std::string& id, double from,
-                                   double to) { return s.p->cost()->summary(scope, id, from, to).dump(); })
+                                   double to) { return s.p->cost()->summary(scope, id, from, to).dump(); }, py::call_guard<py::gil_scoped_release>())
       .def("recommendations_json", [](PyPlatform& s, const std::string& scope, const std::string& id) {
         return list_json(s.p->cost()->recommendations(scope, id));
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("chargeback_json", [](PyPlatform& s, const std::string& by, double from, double to) {
         return s.p->cost()->chargeback(by, from, to).dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("admit", [](PyPlatform& s, const std::string& ns, const std::string& team, const std::string& project,
                        double est, double now) {
         Admission a = s.p->cost()->admit(ns, team, project, est, now);
@@ -416,7 +448,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
         j["throttled"] = a.throttled;
         j["reason"] = a.reason;
         return j.dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("pricing_json", [](PyPlatform& s) {
         Json a = Json::array();
         for (const auto& p : s.p->cost()->pricing_table()) {
@@ -431,7 +463,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
           a.push_back(j);
         }
         return a.dump();
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("set_pricing", [](PyPlatform& s, const std::string& js) {
         Json j = Json::parse(js);
         GpuPricing p;
@@ -441,7 +473,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
         p.reserved = j.get("reserved").as_number();
         for (const auto& kv : j.get("partition").fields()) p.partition[kv.first] = kv.second.as_number();
         s.p->cost()->set_pricing(p);
-      })
+      }, py::call_guard<py::gil_scoped_release>())
       .def("cost_replayed", [](PyPlatform& s) { return s.p->cost()->replayed(); })
       .def("cost_resumed", [](PyPlatform& s) { return s.p->cost()->resumed(); })
       // ---- metrics / housekeeping
@@ -450,6 +482,6 @@ PYBIND11_MODULE(_kgwe_core, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("metric_value", [](PyPlatform& s, const std::string& name, const std::vector<std::string>& labels) {
         return s.p->metrics()->value(name, labels);
-      })
-      .def("metric_families", [](PyPlatform& s) { return s.p->metrics()->families(); });
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("metric_families", [](PyPlatform& s) { return s.p->metrics()->families(); }, py::call_guard<py::gil_scoped_release>());
 }

@@ -36,7 +36,7 @@ void DiscoveryService::add_node(const std::string& name, std::shared_ptr<Hal> ha
   std::lock_guard<std::mutex> lk(publish_mu_);
   auto prev = snapshot();
   auto next = std::make_shared<ClusterTopology>(*prev);
-  next->nodes[name] = std::move(n);
+  next->nodes.set(name, std::move(n));
   publish(next, prev);
 }
 
@@ -61,7 +61,7 @@ void DiscoveryService::upsert_node(const NodeTopology& node) {
   std::lock_guard<std::mutex> lk(publish_mu_);
   auto prev = snapshot();
   auto next = std::make_shared<ClusterTopology>(*prev);
-  next->nodes[node.name] = node;
+  next->nodes.set(node.name, node);
   publish(next, prev);
 }
 
@@ -75,8 +75,8 @@ void DiscoveryService::refresh() {
   }
   // Discovery runs without any lock readers could contend on.
   auto next = std::make_shared<ClusterTopology>();
-  for (auto& kv : hs) next->nodes[kv.first] = kv.second->discover(kv.first);
-  for (auto& kv : pushed) next->nodes[kv.first] = kv.second;
+  for (auto& kv : hs) next->nodes.set(kv.first, kv.second->discover(kv.first));
+  for (auto& kv : pushed) next->nodes.set(kv.first, kv.second);
   std::lock_guard<std::mutex> lk(publish_mu_);
   publish(next, snapshot());
 }
@@ -88,7 +88,7 @@ bool DiscoveryService::refresh_node(const std::string& name) {
   std::lock_guard<std::mutex> lk(publish_mu_);
   auto prev = snapshot();
   auto next = std::make_shared<ClusterTopology>(*prev);
-  next->nodes[name] = std::move(n);
+  next->nodes.set(name, std::move(n));
   publish(next, prev);
   return true;
 }
@@ -103,17 +103,25 @@ void DiscoveryService::refresh_telemetry() {
   auto prev = snapshot();
   auto next = std::make_shared<ClusterTopology>(*prev);
   for (auto& kv : hs) {
-    auto it = next->nodes.find(kv.first);
-    if (it != next->nodes.end()) kv.second->refresh_telemetry(it->second);
+    if (next->nodes.count(kv.first)) {
+      NodeTopology& n = next->nodes.mut(kv.first);
+      kv.second->refresh_telemetry(n);
+      index_links(n);  // telemetry carries link up/down and measured bandwidth
+    }
   }
   publish(next, prev);
 }
 
 void DiscoveryService::publish(std::shared_ptr<ClusterTopology> next, const TopologySnapshot& prev) {
+  std::vector<std::string> unindexed;  // new / re-discovered nodes arrive without link tables
+  for (const auto& kv : next->nodes)
+    if (kv.second.link_bw.size() != kv.second.gpus.size() * kv.second.gpus.size()) unindexed.push_back(kv.first);
+  for (const auto& name : unindexed) index_links(next->nodes.mut(name));
   next->generation = prev->generation + 1;
   next->updated_ns = now_ns();
   // Diff -> events.
   for (const auto& kv : next->nodes) {
+    if (next->nodes.same(kv.first, prev->nodes)) continue;  // untouched node: nothing to diff
     auto pit = prev->nodes.find(kv.first);
     if (pit == prev->nodes.end()) {
       emit({TopologyEventType::NodeAdded, kv.first, "", "", now_ns()});

@@ -44,16 +44,25 @@ MetricRegistry::Family* MetricRegistry::find(const std::string& name) {
   return &it->second;
 }
 
+MetricRegistry::Family* MetricRegistry::find_mut(const std::string& name) {
+  Family* f = find(name);
+  if (f->frozen) {
+    f->series = *f->frozen;
+    f->frozen.reset();
+  }
+  return f;
+}
+
 void MetricRegistry::set(const std::string& name, const Labels& lv, double v) {
   std::lock_guard<std::mutex> lk(mu_);
-  Family* f = find(name);
+  Family* f = find_mut(name);
   if (lv.size() != f->labels.size()) throw std::runtime_error("label arity mismatch for " + name);
   f->series[lv].value = v;
 }
 
 void MetricRegistry::add(const std::string& name, const Labels& lv, double v) {
   std::lock_guard<std::mutex> lk(mu_);
-  Family* f = find(name);
+  Family* f = find_mut(name);
   if (lv.size() != f->labels.size()) throw std::runtime_error("label arity mismatch for " + name);
   if (f->type == MetricType::Counter && v < 0) throw std::runtime_error("counter decrement: " + name);
   f->series[lv].value += v;
@@ -61,7 +70,7 @@ void MetricRegistry::add(const std::string& name, const Labels& lv, double v) {
 
 void MetricRegistry::observe(const std::string& name, const Labels& lv, double v) {
   std::lock_guard<std::mutex> lk(mu_);
-  Family* f = find(name);
+  Family* f = find_mut(name);
   if (f->type != MetricType::Histogram) throw std::runtime_error("not a histogram: " + name);
   if (lv.size() != f->labels.size()) throw std::runtime_error("label arity mismatch for " + name);
   Series& s = f->series[lv];
@@ -77,20 +86,23 @@ void MetricRegistry::observe(const std::string& name, const Labels& lv, double v
 
 void MetricRegistry::remove(const std::string& name, const Labels& lv) {
   std::lock_guard<std::mutex> lk(mu_);
-  find(name)->series.erase(lv);
+  find_mut(name)->series.erase(lv);
 }
 
 void MetricRegistry::clear(const std::string& name) {
   std::lock_guard<std::mutex> lk(mu_);
-  find(name)->series.clear();
+  Family* f = find(name);
+  f->series.clear();
+  f->frozen.reset();
 }
 
 double MetricRegistry::value(const std::string& name, const Labels& lv) const {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = fams_.find(name);
   if (it == fams_.end()) return 0.0;
-  auto s = it->second.series.find(lv);
-  if (s == it->second.series.end()) return 0.0;
+  const SeriesMap& m = it->second.frozen ? *it->second.frozen : it->second.series;
+  auto s = m.find(lv);
+  if (s == m.end()) return 0.0;
   return it->second.type == MetricType::Histogram ? static_cast<double>(s->second.count) : s->second.value;
 }
 
@@ -124,20 +136,33 @@ static std::string label_str(const std::vector<std::string>& names, const std::v
 }
 
 void MetricRegistry::commit(GaugeBatch&& batch) {
-  std::vector<std::pair<std::string, std::map<Labels, Series>>> staged;
+  std::vector<size_t> arity;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& kv : batch.fams_) arity.push_back(find(kv.first)->labels.size());
+  }
+  std::vector<std::pair<std::string, std::shared_ptr<const SeriesMap>>> staged;
   staged.reserve(batch.fams_.size());
+  size_t i = 0;
   for (auto& kv : batch.fams_) {
-    std::map<Labels, Series> series;
-    for (auto& sv : kv.second) series[sv.first].value = sv.second;
+    auto series = std::make_shared<SeriesMap>();
+    auto& m = kv.second;
+    while (!m.empty()) {  // already sorted: move each key to the end, no re-sort, no copy
+      auto nh = m.extract(m.begin());
+      if (nh.key().size() != arity[i]) throw std::runtime_error("label arity mismatch for " + kv.first);
+      Series sr;
+      sr.value = nh.mapped();
+      series->emplace_hint(series->end(), std::move(nh.key()), std::move(sr));
+    }
+    ++i;
     staged.emplace_back(kv.first, std::move(series));
   }
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& st : staged) {
       Family* f = find(st.first);
-      for (const auto& s : st.second)
-        if (s.first.size() != f->labels.size()) throw std::runtime_error("label arity mismatch for " + st.first);
-      f->series.swap(st.second);  // old series are freed below, off the lock
+      f->frozen.swap(st.second);  // old snapshot freed below, off the lock
+      f->series.clear();
     }
   }
 }
@@ -151,11 +176,12 @@ std::string MetricRegistry::expose() const {
   std::string out;
   for (const auto& kv : fams) {
     const Family& f = kv.second;
+    const SeriesMap& series = f.frozen ? *f.frozen : f.series;
     const char* t = f.type == MetricType::Counter ? "counter" : f.type == MetricType::Gauge ? "gauge"
                                                                                             : "histogram";
     out += "# HELP " + kv.first + " " + f.help + "\n";
     out += "# TYPE " + kv.first + " " + t + "\n";
-    for (const auto& s : f.series) {
+    for (const auto& s : series) {
       if (f.type != MetricType::Histogram) {
         out += kv.first + label_str(f.labels, s.first) + " " + prom_number(s.second.value) + "\n";
         continue;

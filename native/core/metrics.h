@@ -53,14 +53,20 @@ class MetricRegistry {
     double sum = 0.0;
     uint64_t count = 0;
   };
+  using SeriesMap = std::map<Labels, Series>;
   struct Family {
     MetricType type;
     std::string help;
     std::vector<std::string> labels;
     std::vector<double> buckets;
-    std::map<Labels, Series> series;
+    SeriesMap series;
+    // Committed by a GaugeBatch: immutable and shared with in-flight scrapes,
+    // so expose() copies a pointer under the lock, not 10^5 series.  A later
+    // set()/add() on the family copies it back into `series` (copy-on-write).
+    std::shared_ptr<const SeriesMap> frozen;
   };
   Family* find(const std::string& name);
+  Family* find_mut(const std::string& name);  // find + thaw a committed family
   mutable std::mutex mu_;
   std::map<std::string, Family> fams_;
 };

@@ -1,8 +1,53 @@
 #include "model.h"
 
+#include <cstring>
+#include <functional>
+
 #include <chrono>
 
 namespace kgwe {
+
+void index_links(NodeTopology& n) {
+  const size_t G = n.gpus.size();
+  n.link_bw.assign(G * G, 0.0f);
+  n.link_up.assign(G * G, 0);
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over everything placement reads
+  auto mix = [&h](uint64_t v) {
+    h ^= v;
+    h *= 1099511628211ull;
+  };
+  mix(G);
+  for (size_t i = 0; i < G; ++i) {
+    const GpuDevice& a = n.gpus[i];
+    mix(static_cast<uint64_t>(a.numa_node + 7));
+    mix(std::hash<std::string>{}(a.pcie.switch_id));
+    mix(a.healthy() ? 1 : 2);
+    for (size_t j = 0; j < G; ++j) {
+      if (i == j) continue;
+      const GpuDevice& b = n.gpus[j];
+      const XgmiLink* l1 = a.link_to(b.uuid);
+      const XgmiLink* l2 = b.link_to(a.uuid);
+      const bool up1 = l1 && l1->up && l1->type == LinkType::XGMI;
+      const bool up2 = l2 ? (l2->up && l2->type == LinkType::XGMI) : up1;
+      double bw;
+      if (up1 && up2) {
+        bw = l1->effective_gbps();
+        if (l2) bw = std::min(bw, l2->effective_gbps());
+      } else {
+        bw = std::min(a.pcie.bandwidth_gbps, b.pcie.bandwidth_gbps);
+      }
+      n.link_bw[i * G + j] = static_cast<float>(bw);
+      n.link_up[i * G + j] = up1 && up2;
+      uint32_t bits;
+      const float fb = static_cast<float>(bw);
+      std::memcpy(&bits, &fb, sizeof bits);
+      mix(bits ^ (static_cast<uint64_t>(up1 && up2) << 32));
+      // degraded-link count input of the 1-GPU best fit
+      if (l1) mix((l1->up ? 3 : 5) ^ static_cast<uint64_t>(l1->measured_gbps * 16));
+    }
+  }
+  n.topo_fp = h ? h : 1;
+}
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(

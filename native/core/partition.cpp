@@ -141,13 +141,15 @@ bool PartitionController::gpu_idle(const GpuDevice& g) const {
 }
 
 int PartitionController::free_slices(const ClusterTopology& c, ComputePartition mode,
-                                     const MemoryPartition* memory) const {
+                                     const MemoryPartition* memory,
+                                     const std::unordered_set<std::string>* within) const {
   int n = 0;
   std::set<std::string> owned;  // slices held in the ledger (one pass, not per slice)
   if (sched_)
     for (const auto& a : sched_->allocations())
       for (const auto& p : a.partitions) owned.insert(p);
-  for (const auto& kv : c.nodes)
+  for (const auto& kv : c.nodes) {
+    if (within && !within->count(kv.first)) continue;
     for (const auto& g : kv.second.gpus) {
       if (g.partition.compute != mode || !g.healthy() || g.partition.switching) continue;
       if (memory && g.partition.memory != *memory) continue;
@@ -155,6 +157,7 @@ int PartitionController::free_slices(const ClusterTopology& c, ComputePartition 
       for (const auto& pi : g.partition.instances)
         n += (pi.in_use || owned.count(pi.id)) ? 0 : 1;
     }
+  }
   return n;
 }
 
@@ -217,11 +220,12 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
 }
 
 std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition mode, int count,
-                                                              bool plan_only, const MemoryPartition* memory) {
+                                                              bool plan_only, const MemoryPartition* memory,
+                                                              const std::unordered_set<std::string>* within) {
   std::vector<PartitionOp> out;
   if (memory && !valid_mode_combo(mode, *memory)) return out;
   auto snap = disc_->snapshot();
-  int have = free_slices(*snap, mode, memory);
+  int have = free_slices(*snap, mode, memory, within);
   if (have >= count) return out;
   const int per_gpu = partition_count(mode);
   // Candidate idle GPUs in a different mode; prefer nodes already running the
@@ -234,6 +238,7 @@ std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition m
   };
   std::vector<Cand> cands;
   for (const auto& kv : snap->nodes) {
+    if (within && !within->count(kv.first)) continue;
     int has_mode = 0, idle = 0;
     for (const auto& g : kv.second.gpus) {
       has_mode += g.partition.compute == mode;

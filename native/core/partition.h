@@ -26,6 +26,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "discovery.h"
@@ -103,8 +104,12 @@ class PartitionController {
   // slices of `mode` exist.  Returns the operations (possibly empty).
   // `memory` (optional): the NPS mode the slices must have; converted GPUs
   // are switched to it too.
+  // `within` (optional): only count and convert GPUs on these nodes — the
+  // extender passes the pod's candidate nodes, so capacity appears where
+  // kube-scheduler can actually bind.
   std::vector<PartitionOp> ensure_capacity(ComputePartition mode, int count, bool plan_only = false,
-                                           const MemoryPartition* memory = nullptr);
+                                           const MemoryPartition* memory = nullptr,
+                                           const std::unordered_set<std::string>* within = nullptr);
   // Move idle GPUs toward a strategy's distribution.
   std::vector<PartitionOp> rebalance(const std::string& strategy, bool plan_only = false);
   // Return idle partitioned GPUs with no slice in use back to SPX.
@@ -134,7 +139,8 @@ class PartitionController {
   bool gpu_idle(const GpuDevice& g) const;
   PartitionOp execute(const std::string& node, const GpuDevice& g, ComputePartition to,
                       const std::string& reason, bool plan_only, const MemoryPartition* mem_to = nullptr);
-  int free_slices(const ClusterTopology& c, ComputePartition mode, const MemoryPartition* memory = nullptr) const;
+  int free_slices(const ClusterTopology& c, ComputePartition mode, const MemoryPartition* memory = nullptr,
+                  const std::unordered_set<std::string>* within = nullptr) const;
 
   std::shared_ptr<DiscoveryService> disc_;
   std::shared_ptr<Scheduler> sched_;

@@ -1,8 +1,11 @@
 #include "platform.h"
 
+#include "extender_scan.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <set>
 
 namespace kgwe {
 
@@ -215,27 +218,79 @@ size_t Platform::queue_depth() const {
 }
 
 std::string Platform::filter(const std::string& body) {
-  Json out = Json::object();
-  Json args;
+  // Fast path: zero-copy scan (names + byte spans of the Node items); the
+  // reply splices the passing items' original bytes.  Fallback: full parse.
+  ExtenderArgsScan scan;
+  bool scanned = false;
   try {
-    args = Json::parse(body);
-  } catch (const std::exception& e) {
-    out["error"] = std::string("bad ExtenderArgs: ") + e.what();
-    return out.dump();
+    scanned = scan_extender_args(body, &scan);
+  } catch (...) {
+    scanned = false;
   }
-  const Json& pod = field(args, "pod", "Pod");
+  Json parsed;
+  if (!scanned) {
+    Json out = Json::object();
+    try {
+      parsed = Json::parse(body);
+    } catch (const std::exception& e) {
+      out["error"] = std::string("bad ExtenderArgs: ") + e.what();
+      return out.dump();
+    }
+    scan = ExtenderArgsScan();
+    scan.pod = field(parsed, "pod", "Pod");
+    const Json& nodes = field(parsed, "nodes", "Nodes");
+    scan.have_nodes = nodes.is_object();
+    for (const auto& n : nodes.get("items").items()) {
+      NodeSpan ns;
+      ns.name = n.get("metadata").get("name").str();
+      scan.nodes.push_back(ns);
+    }
+    for (const auto& n : field(parsed, "nodenames", "NodeNames").items()) scan.nodenames.push_back(n.str());
+  }
+  const Json& pod = scan.pod;
   WorkloadRequest w = workload_from_pod(pod, cfg_.gpu_resource);
   // Microsecond creation stamp written by kgwe's mutating webhook (the
   // apiserver's creationTimestamp is whole seconds); else first filter call.
   remember_pod(w.uid, w,
                std::atof(pod.get("metadata").get("annotations").get("kgwe.amd.com/created-at").str("0").c_str()));
   std::vector<std::string> names;
-  const Json& nodes = field(args, "nodes", "Nodes");
-  const bool full_nodes = nodes.is_object();
-  for (const auto& n : nodes.get("items").items()) names.push_back(n.get("metadata").get("name").str());
-  for (const auto& n : field(args, "nodenames", "NodeNames").items()) names.push_back(n.str());
+  names.reserve(scan.nodes.size() + scan.nodenames.size());
+  for (const auto& n : scan.nodes) names.push_back(n.name);
+  for (const auto& n : scan.nodenames) names.push_back(n);
   Json failed = Json::object();
   std::vector<std::string> passed;
+  auto reply = [&]() {
+    std::string out = "{\"failedNodes\":";
+    failed.dump_to(out);
+    if (scan.have_nodes) {
+      std::set<std::string> ok(passed.begin(), passed.end());
+      out += ",\"nodes\":{\"items\":[";
+      bool first = true;
+      if (scanned) {
+        for (const auto& n : scan.nodes)
+          if (ok.count(n.name)) {
+            if (!first) out += ',';
+            out.append(body, n.begin, n.end - n.begin);
+            first = false;
+          }
+      } else {
+        for (const auto& n : field(parsed, "nodes", "Nodes").get("items").items())
+          if (ok.count(n.get("metadata").get("name").str())) {
+            if (!first) out += ',';
+            n.dump_to(out);
+            first = false;
+          }
+      }
+      out += "]}";
+    } else {
+      Json nn = Json::array();
+      for (const auto& n : passed) nn.push_back(n);
+      out += ",\"nodenames\":";
+      nn.dump_to(out);
+    }
+    out += "}";
+    return out;
+  };
   if (cfg_.enforce_budgets) {
     // Estimate: one hour of this request at on-demand prices.
     const GpuPricing p = cost_->pricing("amd-mi355x-288gb");
@@ -244,16 +299,15 @@ std::string Platform::filter(const std::string& body) {
     Admission a = cost_->admit(w.ns, w.team, w.project, est, wall_s());
     if (!a.allowed) {
       for (const auto& n : names) failed[n] = a.reason;
-      out["failedNodes"] = failed;
-      out["nodenames"] = Json::array();
       reg_->add("kgwe_scheduling_failures_total", {"budget"}, 1);
-      return out.dump();
+      return reply();
     }
   }
   auto fails = sched_->filter(w, names, &passed);
   if (passed.empty() && w.partition && cfg_.auto_provision_partitions) {
+    const std::unordered_set<std::string> cand(names.begin(), names.end());
     auto ops = part_->ensure_capacity(w.partition_mode, w.partition_count, false,
-                                      w.partition_memory_set ? &w.partition_memory : nullptr);
+                                      w.partition_memory_set ? &w.partition_memory : nullptr, &cand);
     for (const auto& op : ops)
       reg_->add("kgwe_partition_reconfigurations_total",
                 {op.node, op.state == OpState::Failed ? "failed" : "ok"}, 1);
@@ -263,37 +317,38 @@ std::string Platform::filter(const std::string& body) {
     }
   }
   for (const auto& kv : fails) failed[kv.first] = kv.second;
-  out["failedNodes"] = failed;
-  if (full_nodes) {
-    Json items = Json::array();
-    for (const auto& n : nodes.get("items").items())
-      if (std::find(passed.begin(), passed.end(), n.get("metadata").get("name").str()) != passed.end())
-        items.push_back(n);
-    Json nl = Json::object();
-    nl["items"] = items;
-    out["nodes"] = nl;
-  } else {
-    Json nn = Json::array();
-    for (const auto& n : passed) nn.push_back(n);
-    out["nodenames"] = nn;
-  }
   if (passed.empty()) reg_->add("kgwe_scheduling_failures_total", {"filter"}, 1);
-  return out.dump();
+  return reply();
 }
 
 std::string Platform::prioritize(const std::string& body) {
-  Json args;
+  ExtenderArgsScan scan;
+  bool scanned = false;
   try {
-    args = Json::parse(body);
+    scanned = scan_extender_args(body, &scan);
   } catch (...) {
-    return "[]";
+    scanned = false;
   }
-  const Json& pod = field(args, "pod", "Pod");
-  WorkloadRequest w = workload_from_pod(pod, cfg_.gpu_resource);
+  if (!scanned) {
+    Json args;
+    try {
+      args = Json::parse(body);
+    } catch (...) {
+      return "[]";
+    }
+    scan = ExtenderArgsScan();
+    scan.pod = field(args, "pod", "Pod");
+    for (const auto& n : field(args, "nodes", "Nodes").get("items").items()) {
+      NodeSpan ns;
+      ns.name = n.get("metadata").get("name").str();
+      scan.nodes.push_back(ns);
+    }
+    for (const auto& n : field(args, "nodenames", "NodeNames").items()) scan.nodenames.push_back(n.str());
+  }
+  WorkloadRequest w = workload_from_pod(scan.pod, cfg_.gpu_resource);
   std::vector<std::string> names;
-  for (const auto& n : field(args, "nodes", "Nodes").get("items").items())
-    names.push_back(n.get("metadata").get("name").str());
-  for (const auto& n : field(args, "nodenames", "NodeNames").items()) names.push_back(n.str());
+  for (const auto& n : scan.nodes) names.push_back(n.name);
+  for (const auto& n : scan.nodenames) names.push_back(n);
   Json out = Json::array();
   for (const auto& s : sched_->prioritize(w, names)) {
     Json h = Json::object();
@@ -302,6 +357,38 @@ std::string Platform::prioritize(const std::string& body) {
     h["score"] = static_cast<int64_t>(std::min(10.0, std::round(s.total / 10.0)));
     out.push_back(h);
   }
+  return out.dump();
+}
+
+std::string Platform::preempt(const std::string& body) {
+  Json args;
+  Json out = Json::object();
+  try {
+    args = Json::parse(body);
+  } catch (const std::exception& e) {
+    out["error"] = std::string("bad ExtenderPreemptionArgs: ") + e.what();
+    return out.dump();
+  }
+  WorkloadRequest w = workload_from_pod(field(args, "pod", "Pod"), cfg_.gpu_resource);
+  std::vector<std::string> names;
+  for (const auto& kv : field(args, "nodeNameToMetaVictims", "NodeNameToMetaVictims").fields())
+    names.push_back(kv.first);
+  for (const auto& kv : field(args, "nodeNameToVictims", "NodeNameToVictims").fields())
+    if (std::find(names.begin(), names.end(), kv.first) == names.end()) names.push_back(kv.first);
+  Json res = Json::object();
+  for (const auto& kv : sched_->preemption_plans(w, names)) {
+    Json mv = Json::object();
+    Json pods = Json::array();
+    for (const auto& uid : kv.second) {
+      Json p = Json::object();
+      p["uid"] = uid;
+      pods.push_back(p);
+    }
+    mv["pods"] = pods;
+    mv["numPDBViolations"] = static_cast<int64_t>(0);
+    res[kv.first] = mv;
+  }
+  out["nodeNameToMetaVictims"] = res;
   return out.dump();
 }
 
@@ -502,7 +589,12 @@ void Platform::tick(double now_s) {
   }
   if (cfg_.partition_reclaim_idle_s >= 0)
     part_->reclaim_idle_after(now_s, cfg_.partition_reclaim_idle_s);
-  refresh_gauges(now_s);
+  const int64_t t0 = now_ns();
+  if (t0 >= gauges_next_ns_.load()) {
+    refresh_gauges(now_s);
+    const int64_t t1 = now_ns();
+    gauges_next_ns_.store(t1 + 9 * (t1 - t0));
+  }
 }
 
 void Platform::refresh_gauges(double now_s) {

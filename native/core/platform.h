@@ -17,6 +17,7 @@
 // The HTTP socket handling lives in the Python shell (kgwe/extender); every
 // byte of request parsing, scoring and response building is here.
 #pragma once
+#include <atomic>
 #include <memory>
 #include <string>
 
@@ -66,6 +67,10 @@ class Platform {
   // Extender verbs (bodies are JSON text).
   std::string filter(const std::string& body);
   std::string prioritize(const std::string& body);
+  // ExtenderPreemptionArgs -> ExtenderPreemptionResult (nodeNameToMetaVictims):
+  // the victims kube-scheduler should evict per node so the pod fits on
+  // kgwe's terms (whole gangs, share clients, priorities, preemptible).
+  std::string preempt(const std::string& body);
   // Returns {"result": ExtenderBindingResult, "placement": {...}}.
   std::string bind(const std::string& body, const std::string& pod_json = "");
 
@@ -109,6 +114,9 @@ class Platform {
   // pods not yet bound: the latency origin and the queue.
   std::map<std::string, std::pair<int64_t, double>> pending_;
   LatencyHistogram pod_latency_;
+  // tick() refreshes gauges at most at a 10 % duty cycle: at 10,000 GPUs a
+  // refresh is ~0.5 s of CPU, and a scrape refreshes them anyway.
+  std::atomic<int64_t> gauges_next_ns_{0};
 };
 
 }  // namespace kgwe

@@ -7,6 +7,9 @@
 
 namespace kgwe {
 
+constexpr size_t kSweepChunk = 32;  // nodes per shared-lock hold in filter / prioritize
+
+
 // ---------------------------------------------------------------------------
 // enums
 // ---------------------------------------------------------------------------
@@ -427,7 +430,7 @@ Scheduler::Scheduler(std::shared_ptr<DiscoveryService> disc, SchedulerConfig cfg
     : disc_(std::move(disc)), cfg_(cfg) {}
 
 void Scheduler::set_config(const SchedulerConfig& c) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   cfg_ = c;
 }
 
@@ -549,10 +552,67 @@ std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w)
   return "";
 }
 
-// xGMI-aware group selection + topology score (see header).
+// Memo of group searches.  A search's result depends only on the node's
+// topology (links, NUMA, switches, health: NodeTopology::topo_fp), WHICH GPUs
+// are free, the request size / preference and the scorer config — on a fleet
+// of identical 8xMI355X nodes a 1,250-node prioritize repeats the same few
+// searches thousands of times.  Thread-local: no lock on the hot path.
+namespace {
+struct TopoMemo {
+  int score = 0;
+  std::vector<int> positions;  // selected GPUs by position in NodeTopology::gpus
+  double bw = 0.0;
+  bool clique = false;
+};
+thread_local std::unordered_map<uint64_t, TopoMemo> t_topo_memo;
+}  // namespace
+
 int Scheduler::topology_score(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
                               const WorkloadRequest& w, std::vector<std::string>* sel, double* bw_out,
                               bool* clique_out) const {
+  const size_t G = n.gpus.size();
+  const bool indexed = n.topo_fp != 0 && n.link_bw.size() == G * G && G <= 64;
+  uint64_t key = 0;
+  if (indexed) {
+    uint64_t mask = 0;
+    for (auto* g : avail) mask |= 1ull << n.position(g);
+    key = n.topo_fp;
+    auto mix = [&key](uint64_t v) {
+      key ^= v + 0x9e3779b97f4a7c15ull + (key << 6) + (key >> 2);
+    };
+    mix(mask);
+    mix(static_cast<uint64_t>(w.gpu_count));
+    mix(static_cast<uint64_t>(w.topology));
+    mix(static_cast<uint64_t>(cfg_.rated_link_gbps * 1000));
+    mix(static_cast<uint64_t>(cfg_.degraded_link_ratio * 1000));
+    mix(cfg_.exhaustive_limit);
+    auto it = t_topo_memo.find(key);
+    if (it != t_topo_memo.end()) {
+      sel->clear();
+      for (int p : it->second.positions) sel->push_back(n.gpus[p].uuid);
+      *bw_out = it->second.bw;
+      *clique_out = it->second.clique;
+      return it->second.score;
+    }
+  }
+  const int score = topology_search(n, avail, w, sel, bw_out, clique_out);
+  if (indexed) {
+    if (t_topo_memo.size() > 65536) t_topo_memo.clear();
+    TopoMemo mm;
+    mm.score = score;
+    mm.bw = *bw_out;
+    mm.clique = *clique_out;
+    for (const auto& u : *sel)
+      for (size_t p = 0; p < G; ++p)
+        if (n.gpus[p].uuid == u) mm.positions.push_back(static_cast<int>(p));
+    t_topo_memo.emplace(key, std::move(mm));
+  }
+  return score;
+}
+
+int Scheduler::topology_search(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
+                               const WorkloadRequest& w, std::vector<std::string>* sel, double* bw_out,
+                               bool* clique_out) const {
   const int k = w.gpu_count;
   sel->clear();
   *bw_out = 0.0;
@@ -600,10 +660,19 @@ int Scheduler::topology_score(const NodeTopology& n, const std::vector<const Gpu
   // every free GPU as small integers.
   std::vector<double> bwm(static_cast<size_t>(m) * m, 0.0);
   std::vector<char> upm(static_cast<size_t>(m) * m, 0);
+  const size_t G = n.gpus.size();
+  const bool indexed = n.link_bw.size() == G * G;
   for (int i = 0; i < m; ++i)
     for (int j = i + 1; j < m; ++j) {
       bool up = false;
-      const double bw = pair_bw(*avail[i], *avail[j], &up);
+      double bw;
+      if (indexed) {  // dense table built with the snapshot (index_links)
+        const size_t a = static_cast<size_t>(n.position(avail[i])), b = static_cast<size_t>(n.position(avail[j]));
+        bw = n.link_bw[a * G + b];
+        up = n.link_up[a * G + b] != 0;
+      } else {
+        bw = pair_bw(*avail[i], *avail[j], &up);
+      }
       bwm[i * m + j] = bwm[j * m + i] = bw;
       upm[i * m + j] = upm[j * m + i] = up;
     }
@@ -1035,7 +1104,7 @@ bool Scheduler::gpu_has_slice_owner_locked(const std::string& gpu_uuid) const {
 }
 
 bool Scheduler::fence_gpu(const std::string& gpu_uuid) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   if (gpu_owner_.count(gpu_uuid) || gpu_has_slice_owner_locked(gpu_uuid) || fenced_.count(gpu_uuid) ||
       shared_.count(gpu_uuid))
     return false;
@@ -1044,7 +1113,7 @@ bool Scheduler::fence_gpu(const std::string& gpu_uuid) {
 }
 
 void Scheduler::unfence_gpu(const std::string& gpu_uuid) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   fenced_.erase(gpu_uuid);
 }
 
@@ -1182,7 +1251,7 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
     else stats_.failed++;
   };
   {
-    std::shared_lock<std::shared_mutex> lk(mu_);
+    std::shared_lock<RwLock> lk(mu_);
     auto it = allocs_.find(w.uid);
     if (it != allocs_.end()) {  // idempotent re-schedule
       d = decision_from(it->second, 0, it->second.gang_pending ? "Waiting" : "Scheduled");
@@ -1193,7 +1262,7 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
   for (int attempt = 0; attempt < 2; ++attempt) {
     std::vector<NodeScore> scores;
     {
-      std::shared_lock<std::shared_mutex> lk(mu_);
+      std::shared_lock<RwLock> lk(mu_);
       for (const auto& kv : snap->nodes) {
         std::string why = eligible(kv.second, w);
         if (!why.empty()) {
@@ -1210,7 +1279,7 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
     });
     const int tries = std::min<int>(static_cast<int>(scores.size()), std::max(1, cfg_.max_attempts));
     for (int i = 0; i < tries; ++i) {
-      std::unique_lock<std::shared_mutex> lk(mu_);
+      std::unique_lock<RwLock> lk(mu_);
       NodeScore s = scores[i];
       const NodeTopology& n = snap->nodes.at(s.node);
       bool stale = false;
@@ -1257,7 +1326,7 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
       return d;
     }
     if (attempt == 0 && cfg_.enable_preemption && w.priority > 0) {
-      std::unique_lock<std::shared_mutex> lk(mu_);
+      std::unique_lock<RwLock> lk(mu_);
       if (try_preempt(w, snap, &d)) continue;
     }
     break;
@@ -1272,12 +1341,12 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
 // Caller holds mu_ exclusively.  Picks, over all nodes, the cheapest set of
 // lower-priority preemptible allocations whose removal makes the node
 // eligible; cost = (sum of victim priorities, #victims, victim GPUs).
-bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d) {
-  struct Plan {
-    std::string node;
-    std::vector<std::string> victims;
-    std::tuple<int64_t, size_t, size_t> cost{INT64_MAX, 0, 0};
-  } best;
+// Caller holds mu_ exclusively (the ledger is temporarily edited and
+// restored).  The cheapest set of lower-priority preemptible allocations
+// (whole gangs) whose removal makes node `n` eligible for `w`; false if none.
+bool Scheduler::plan_node_preemption(const WorkloadRequest& w, const NodeTopology& n,
+                                     std::vector<std::string>* victims_out,
+                                     std::tuple<int64_t, size_t, size_t>* cost_out) {
   // A gang is preempted as a unit: its other members (on any node) would
   // otherwise keep their GPUs while the job cannot run.
   auto unit_of = [&](const Allocation& a, std::vector<const Allocation*>* out) {
@@ -1292,71 +1361,84 @@ bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& sn
       }
     return true;
   };
-  for (const auto& kv : snap->nodes) {
-    std::vector<const Allocation*> cands;
-    for (const auto& a : allocs_)
-      if (a.second.node == kv.first && a.second.preemptible && a.second.priority < w.priority)
-        cands.push_back(&a.second);
-    if (cands.empty()) continue;
-    std::sort(cands.begin(), cands.end(), [](const Allocation* a, const Allocation* b) {
-      if (a->priority != b->priority) return a->priority < b->priority;
-      return a->allocated_ns > b->allocated_ns;  // youngest first: least work lost
-    });
-    // Temporarily hide victims (whole gangs) one unit at a time until the node
-    // becomes eligible.
-    std::vector<std::string> victims;
-    std::set<std::string> hidden_uids;
-    std::vector<std::pair<std::string, std::string>> hidden_g, hidden_p;
-    std::vector<std::pair<std::string, SharedGpu>> hidden_s;
-    int64_t prio = 0;
-    size_t ngpu = 0;
-    bool ok = false;
-    for (const Allocation* c : cands) {
-      if (hidden_uids.count(c->uid)) continue;
-      std::vector<const Allocation*> unit;
-      if (!unit_of(*c, &unit)) continue;
-      for (const Allocation* a : unit) {
-        if (!hidden_uids.insert(a->uid).second) continue;
-        victims.push_back(a->uid);
-        prio += a->priority;
-        ngpu += a->gpus.size() + a->partitions.size() + (a->shared_gpu.empty() ? 0 : 1);
-        for (const auto& g : a->gpus) {
-          hidden_g.emplace_back(g, gpu_owner_[g]);
-          gpu_owner_.erase(g);
-        }
-        for (const auto& p : a->partitions) {
-          hidden_p.emplace_back(p, part_owner_[p]);
-          part_owner_.erase(p);
-        }
-        if (!a->shared_gpu.empty()) {
-          auto sh = shared_.find(a->shared_gpu);
-          if (sh != shared_.end()) {
-            hidden_s.emplace_back(sh->first, sh->second);
-            auto& cl = sh->second.clients;
-            cl.erase(std::remove(cl.begin(), cl.end(), a->uid), cl.end());
-            if (cl.empty()) shared_.erase(sh);
-          }
-        }
+  std::vector<const Allocation*> cands;
+  for (const auto& a : allocs_)
+    if (a.second.node == n.name && a.second.preemptible && a.second.priority < w.priority)
+      cands.push_back(&a.second);
+  if (cands.empty()) return false;
+  std::sort(cands.begin(), cands.end(), [](const Allocation* a, const Allocation* b) {
+    if (a->priority != b->priority) return a->priority < b->priority;
+    return a->allocated_ns > b->allocated_ns;  // youngest first: least work lost
+  });
+  // Temporarily hide victims (whole gangs) one unit at a time until the node
+  // becomes eligible.
+  std::vector<std::string> victims;
+  std::set<std::string> hidden_uids;
+  std::vector<std::pair<std::string, std::string>> hidden_g, hidden_p;
+  std::vector<std::pair<std::string, SharedGpu>> hidden_s;
+  int64_t prio = 0;
+  size_t ngpu = 0;
+  bool ok = false;
+  for (const Allocation* c : cands) {
+    if (hidden_uids.count(c->uid)) continue;
+    std::vector<const Allocation*> unit;
+    if (!unit_of(*c, &unit)) continue;
+    for (const Allocation* a : unit) {
+      if (!hidden_uids.insert(a->uid).second) continue;
+      victims.push_back(a->uid);
+      prio += a->priority;
+      ngpu += a->gpus.size() + a->partitions.size() + (a->shared_gpu.empty() ? 0 : 1);
+      for (const auto& g : a->gpus) {
+        hidden_g.emplace_back(g, gpu_owner_[g]);
+        gpu_owner_.erase(g);
       }
-      if (eligible(kv.second, w).empty()) {
-        ok = true;
-        break;
+      for (const auto& p : a->partitions) {
+        hidden_p.emplace_back(p, part_owner_[p]);
+        part_owner_.erase(p);
+      }
+      if (!a->shared_gpu.empty()) {
+        auto sh = shared_.find(a->shared_gpu);
+        if (sh != shared_.end()) {
+          hidden_s.emplace_back(sh->first, sh->second);
+          auto& cl = sh->second.clients;
+          cl.erase(std::remove(cl.begin(), cl.end(), a->uid), cl.end());
+          if (cl.empty()) shared_.erase(sh);
+        }
       }
     }
-    for (auto& h : hidden_g) gpu_owner_[h.first] = h.second;
-    for (auto& h : hidden_p) part_owner_[h.first] = h.second;
-    // Restore shares in reverse so the earliest (fullest) snapshot wins.
-    for (auto it = hidden_s.rbegin(); it != hidden_s.rend(); ++it) shared_[it->first] = it->second;
-    if (!ok) continue;
-    std::tuple<int64_t, size_t, size_t> cost{prio, victims.size(), ngpu};
-    if (cost < best.cost) {
-      best.node = kv.first;
-      best.victims = victims;
-      best.cost = cost;
+    if (eligible(n, w).empty()) {
+      ok = true;
+      break;
     }
   }
-  if (best.node.empty()) return false;
-  for (const auto& uid : best.victims) {
+  for (auto& h : hidden_g) gpu_owner_[h.first] = h.second;
+  for (auto& h : hidden_p) part_owner_[h.first] = h.second;
+  // Restore shares in reverse so the earliest (fullest) snapshot wins.
+  for (auto it = hidden_s.rbegin(); it != hidden_s.rend(); ++it) shared_[it->first] = it->second;
+  if (!ok) return false;
+  *victims_out = std::move(victims);
+  *cost_out = {prio, victims_out->size(), ngpu};
+  return true;
+}
+
+// Caller holds mu_ exclusively.  Picks, over all nodes, the cheapest victim
+// set; cost = (sum of victim priorities, #victims, victim GPUs).
+bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d) {
+  std::string best_node;
+  std::vector<std::string> best;
+  std::tuple<int64_t, size_t, size_t> best_cost{INT64_MAX, 0, 0};
+  for (const auto& kv : snap->nodes) {
+    std::vector<std::string> victims;
+    std::tuple<int64_t, size_t, size_t> cost;
+    if (!plan_node_preemption(w, kv.second, &victims, &cost)) continue;
+    if (cost < best_cost) {
+      best_node = kv.first;
+      best = std::move(victims);
+      best_cost = cost;
+    }
+  }
+  if (best_node.empty()) return false;
+  for (const auto& uid : best) {
     auto it = allocs_.find(uid);
     if (it == allocs_.end()) continue;
     const std::string gang = it->second.gang;
@@ -1373,15 +1455,40 @@ bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& sn
     emit({SchedEventType::Preempted, uid, node, "by " + w.uid, now_ns()});
   }
   std::lock_guard<std::mutex> sl(stat_mu_);
-  stats_.preemptions += best.victims.size();
+  stats_.preemptions += best.size();
   return true;
+}
+
+std::map<std::string, std::vector<std::string>> Scheduler::preemption_plans(
+    const WorkloadRequest& w, const std::vector<std::string>& nodes) {
+  std::map<std::string, std::vector<std::string>> out;
+  if (!cfg_.enable_preemption || w.priority <= 0) return out;
+  auto snap = disc_->snapshot();
+  std::unique_lock<RwLock> lk(mu_);  // plans edit (and restore) the ledger
+  for (const auto& name : nodes) {
+    auto it = snap->nodes.find(name);
+    if (it == snap->nodes.end()) continue;
+    if (eligible(it->second, w).empty()) {
+      out[name] = {};  // fits without victims
+      continue;
+    }
+    std::vector<std::string> victims;
+    std::tuple<int64_t, size_t, size_t> cost;
+    if (plan_node_preemption(w, it->second, &victims, &cost)) out[name] = std::move(victims);
+  }
+  return out;
+}
+
+void Scheduler::count_preemptions(size_t n) {
+  std::lock_guard<std::mutex> sl(stat_mu_);
+  stats_.preemptions += n;
 }
 
 std::vector<Decision> Scheduler::schedule_gang(const std::vector<WorkloadRequest>& members) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<Decision> out;
   auto snap = disc_->snapshot();
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   std::vector<std::string> placed;
   bool ok = true;
   auto fill = [](Decision& d, const NodeScore& s) {
@@ -1515,9 +1622,18 @@ std::map<std::string, std::string> Scheduler::filter(const WorkloadRequest& w,
                                                      std::vector<std::string>* passed) {
   std::map<std::string, std::string> failed;
   auto snap = disc_->snapshot();
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  // The ledger is read in chunks of kSweepChunk nodes: a sweep over 1,250
+  // candidates must not hold binds / releases off the ledger for its whole
+  // length (each node's verdict is advisory anyway: bind re-checks).
+  std::shared_lock<RwLock> lk(mu_);
   auto mine = allocs_.find(w.uid);
+  size_t k = 0;
   for (const auto& name : nodes) {
+    if (++k % kSweepChunk == 0) {
+      lk.unlock();
+      lk.lock();
+      mine = allocs_.find(w.uid);
+    }
     auto it = snap->nodes.find(name);
     if (it == snap->nodes.end()) {
       failed[name] = "node not managed by kgwe (no MI355X topology)";
@@ -1538,9 +1654,15 @@ std::map<std::string, std::string> Scheduler::filter(const WorkloadRequest& w,
 std::vector<NodeScore> Scheduler::prioritize(const WorkloadRequest& w,
                                              const std::vector<std::string>& nodes) {
   std::vector<NodeScore> out;
+  out.reserve(nodes.size());
   auto snap = disc_->snapshot();
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
+  size_t k = 0;
   for (const auto& name : nodes) {
+    if (++k % kSweepChunk == 0) {  // see filter()
+      lk.unlock();
+      lk.lock();
+    }
     auto it = snap->nodes.find(name);
     NodeScore s;
     s.node = name;
@@ -1557,7 +1679,7 @@ Decision Scheduler::bind(const WorkloadRequest& w, const std::string& node) {
   d.uid = w.uid;
   auto snap = disc_->snapshot();
   auto it = snap->nodes.find(node);
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   auto mine = allocs_.find(w.uid);
   if (mine != allocs_.end()) {
     if (mine->second.node != node) {
@@ -1616,7 +1738,7 @@ Decision Scheduler::bind(const WorkloadRequest& w, const std::string& node) {
 
 std::string Scheduler::permit(const std::string& uid) {
   expire_gangs();
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
   auto it = allocs_.find(uid);
   if (it == allocs_.end()) return "Reject";
   if (it->second.gang.empty() || !it->second.gang_pending) return "Allow";
@@ -1628,7 +1750,7 @@ std::string Scheduler::permit(const std::string& uid) {
 void Scheduler::expire_gangs() {
   std::vector<std::string> expired;
   {
-    std::unique_lock<std::shared_mutex> lk(mu_);
+    std::unique_lock<RwLock> lk(mu_);
     const int64_t now = now_ns();
     for (auto it = gangs_.begin(); it != gangs_.end();) {
       Gang& g = it->second;
@@ -1655,7 +1777,7 @@ void Scheduler::expire_gangs() {
 bool Scheduler::release(const std::string& uid) {
   std::string node;
   {
-    std::unique_lock<std::shared_mutex> lk(mu_);
+    std::unique_lock<RwLock> lk(mu_);
     auto it = allocs_.find(uid);
     if (it == allocs_.end()) return false;
     node = it->second.node;
@@ -1675,7 +1797,7 @@ bool Scheduler::release(const std::string& uid) {
 }
 
 bool Scheduler::restore(const Allocation& a) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   if (allocs_.count(a.uid)) return false;
   for (const auto& g : a.gpus)
     if (gpu_owner_.count(g) || shared_.count(g)) return false;
@@ -1711,7 +1833,7 @@ bool Scheduler::restore(const Allocation& a) {
 bool Scheduler::migrate_partition(const std::string& uid, const std::string& from, const std::string& to) {
   std::string node;
   {
-    std::unique_lock<std::shared_mutex> lk(mu_);
+    std::unique_lock<RwLock> lk(mu_);
     auto it = allocs_.find(uid);
     if (it == allocs_.end()) return false;
     auto& parts = it->second.partitions;
@@ -1747,7 +1869,7 @@ Decision Scheduler::reserve_share(const WorkloadRequest& w, const std::string& n
     d.failed_nodes[node] = g ? "not a CoLocate / TimeSlice request" : "unknown gpu " + gpu;
     return d;
   }
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::unique_lock<RwLock> lk(mu_);
   if (allocs_.count(w.uid)) {
     d.failed_nodes[node] = "already allocated: " + w.uid;
     return d;
@@ -1770,13 +1892,13 @@ Decision Scheduler::reserve_share(const WorkloadRequest& w, const std::string& n
 }
 
 int Scheduler::share_clients(const std::string& gpu_uuid) const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
   auto it = shared_.find(gpu_uuid);
   return it == shared_.end() ? 0 : static_cast<int>(it->second.clients.size());
 }
 
 bool Scheduler::gpu_busy(const GpuDevice& g) const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
   if (gpu_owner_.count(g.uuid) || shared_.count(g.uuid)) return true;
   for (const auto& pi : g.partition.instances)
     if (part_owner_.count(pi.id)) return true;
@@ -1784,7 +1906,7 @@ bool Scheduler::gpu_busy(const GpuDevice& g) const {
 }
 
 std::vector<Allocation> Scheduler::allocations() const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
   std::vector<Allocation> out;
   out.reserve(allocs_.size());
   for (const auto& kv : allocs_) out.push_back(kv.second);
@@ -1793,7 +1915,7 @@ std::vector<Allocation> Scheduler::allocations() const {
 }
 
 bool Scheduler::allocation(const std::string& uid, Allocation* out) const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
   auto it = allocs_.find(uid);
   if (it == allocs_.end()) return false;
   if (out) *out = it->second;
@@ -1811,7 +1933,7 @@ SchedulerMetrics Scheduler::metrics() const {
   m.p90_ms = latency_.quantile_ms(0.90);
   m.p99_ms = latency_.quantile_ms(0.99);
   m.max_ms = latency_.max_ms();
-  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::shared_lock<RwLock> lk(mu_);
   m.active_allocations = allocs_.size();
   m.allocated_gpus = gpu_owner_.size();
   m.allocated_partitions = part_owner_.size();

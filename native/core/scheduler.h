@@ -34,9 +34,11 @@
 #include <set>
 #include <shared_mutex>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
+#include "rwlock.h"
 #include "discovery.h"
 #include "histogram.h"
 #include "model.h"
@@ -216,6 +218,11 @@ class Scheduler {
   std::vector<NodeScore> prioritize(const WorkloadRequest& w, const std::vector<std::string>& nodes);
   // Reserve on a given node (bind verb); honours gangs (may return Waiting).
   Decision bind(const WorkloadRequest& w, const std::string& node);
+  // Extender preempt verb: per candidate node, the cheapest victim set that
+  // makes room for `w` (empty = fits as is; absent = impossible).  Dry run.
+  std::map<std::string, std::vector<std::string>> preemption_plans(const WorkloadRequest& w,
+                                                                   const std::vector<std::string>& nodes);
+  void count_preemptions(size_t n);
   // Permit-stage check for a gang member: "Allow" | "Wait" | "Reject".
   std::string permit(const std::string& uid);
 
@@ -269,6 +276,8 @@ class Scheduler {
   int topology_score(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
                      const WorkloadRequest& w, std::vector<std::string>* sel, double* bw,
                      bool* clique) const;
+  int topology_search(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
+                      const WorkloadRequest& w, std::vector<std::string>* sel, double* bw, bool* clique) const;
   int topology_score_compat(const NodeTopology& n, const std::vector<const GpuDevice*>& avail,
                             const WorkloadRequest& w, std::vector<std::string>* sel) const;
   int resource_score(const std::vector<const GpuDevice*>& avail, const WorkloadRequest& w) const;
@@ -279,13 +288,15 @@ class Scheduler {
   bool reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending);
   void erase_locked(std::unordered_map<std::string, Allocation>::iterator it);
   bool try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d);
+  bool plan_node_preemption(const WorkloadRequest& w, const NodeTopology& n, std::vector<std::string>* victims,
+                            std::tuple<int64_t, size_t, size_t>* cost);
   void emit(SchedEvent e);
   double bandwidth_of(const NodeTopology& n, const std::vector<std::string>& gpus) const;
 
   std::shared_ptr<DiscoveryService> disc_;
   SchedulerConfig cfg_;
 
-  mutable std::shared_mutex mu_;  // guards the ledger below
+  mutable RwLock mu_;  // guards the ledger below (writer-preferring)
   std::unordered_map<std::string, Allocation> allocs_;
   std::unordered_map<std::string, std::string> gpu_owner_;   // gpu uuid -> uid
   std::unordered_map<std::string, std::string> part_owner_;  // partition id -> uid

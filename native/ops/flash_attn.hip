@@ -42,6 +42,12 @@
 //   * delta = rowsum(dO * O) by a small preprocess kernel.
 #include "common.h"
 
+#include <algorithm>
+#include <array>
+#include <map>
+#include <mutex>
+#include <vector>
+
 using namespace kgwe;
 
 namespace {
@@ -444,18 +450,38 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ delta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S,
-    int Hq, int Hkv, float c, float scale, int causal, int nKB) {
+    int Hq, int Hkv, float c, float scale, int causal, int nKB, const int4* __restrict__ jobs,
+    float* __restrict__ part, int B) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * QTILE];
   __shared__ __attribute__((aligned(16))) bf16_t Ds[2 * QTILE];
   __shared__ __attribute__((aligned(16))) bf16_t Vw[128 * HD];  // this WG's 128 keys
   __shared__ __attribute__((aligned(16))) float Ls[2 * BQT];
   __shared__ __attribute__((aligned(16))) float Dl[2 * BQT];
   const int G = Hq / Hkv;
-  // Decode (b, hkv, key block): XCD-aware, heaviest (earliest keys) first.
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int kb = wg % nKB;
-  const int hkv = (wg / nKB) % Hkv;
-  const int b = wg / (nKB * Hkv);
+  const int nqt = (S + BQT - 1) / BQT;
+  int b, hkv, kb, it0, it1, slot;
+  if (jobs) {
+    // Planned job (kgwe_fa_bwd_plan): a key block, or one half of a heavy
+    // causal key block's (query tile x head) sweep, in longest-first order
+    // per XCD.  Half-jobs write fp32 partials that fa_bwd_dkdv_finalize sums.
+    const int4 jb = jobs[blockIdx.x];
+    if (jb.z >= jb.w) return;  // padding: the whole workgroup leaves before any barrier
+    hkv = jb.x % Hkv;
+    b = jb.x / Hkv;
+    kb = jb.y & 0xffffff;
+    slot = jb.y >> 24;
+    it0 = jb.z;
+    it1 = jb.w;
+  } else {
+    // Decode (b, hkv, key block): XCD-aware, heaviest (earliest keys) first.
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    kb = wg % nKB;
+    hkv = (wg / nKB) % Hkv;
+    b = wg / (nKB * Hkv);
+    slot = 0;
+    it0 = 0;
+    it1 = G * (nqt - (causal ? (kb * 128) / BQT : 0));
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lk = lane & 31, hh = lane >> 5;
   const int key0 = kb * 128 + w * 32;
@@ -482,9 +508,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i) dka[i] = dva[i] = f32x16{};
 
-  const int qt_begin = causal ? (kb * 128) / BQT : 0;
-  const int nqt = (S + BQT - 1) / BQT;
-  const int total = G * (nqt - qt_begin);
+  const int total = it1 - it0;
   // Staging: thread t moves row chunks (r, ch) = ((t + 256 i) >> 4, t & 15), i = 0, 1.
   const int sr = threadIdx.x >> 4, sch = threadIdx.x & 15;
   bf16x8 qr[2], dr[2];
@@ -520,11 +544,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     }
   };
   const AOffs ao = make_aoffs(lane);
+  // Iteration it = (query tile nqt-1 - it/G, head it%G), from it0.
+  int qt = nqt - 1 - it0 / G, g_cur = it0 % G;
   if (total > 0) {
-    gload(0, nqt - 1);
+    gload(g_cur, qt);
     swrite(0);
   }
-  int qt = nqt - 1, g_cur = 0;
   __syncthreads();
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
@@ -588,7 +613,26 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     qt = qt_nxt;
     g_cur = g_nxt;
   }
-  if (EVEN || key < S) {
+  if (slot > 0 && (EVEN || key < S)) {
+    // fp32 partial [slot-1][dk|dv][b][hkv][key][d]
+    const size_t plane = static_cast<size_t>(B) * Hkv * S * HD;
+    float* pk = part + (static_cast<size_t>(slot - 1) * 2) * plane +
+                ((static_cast<size_t>(b) * Hkv + hkv) * S + key) * HD;
+    float* pv = pk + plane;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4 a, bb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = dka[db][4 * g4 + j];
+          bb[j] = dva[db][4 * g4 + j];
+        }
+        *reinterpret_cast<f32x4*>(pk + db * 32 + 8 * g4 + 4 * hh) = a;
+        *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g4 + 4 * hh) = bb;
+      }
+  } else if (EVEN || key < S) {
     const size_t off = (static_cast<size_t>(b) * S + key) * kvs + static_cast<size_t>(hkv) * HD;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
@@ -604,6 +648,36 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
         *reinterpret_cast<u16x4*>(dv + off + db * 32 + 8 * g4 + 4 * hh) = bb;
       }
   }
+}
+
+// Sum the two fp32 halves of every split key block: dK (x scale) and dV to
+// bf16.  One thread = 4 consecutive d of one key; keys [0, split_keys).
+__global__ __launch_bounds__(256) void fa_bwd_dkdv_finalize(const float* __restrict__ part,
+                                                            bf16_t* __restrict__ dk,
+                                                            bf16_t* __restrict__ dv, int B, int S,
+                                                            int Hkv, int split_keys, float scale) {
+  const long long idx = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long per_gh = static_cast<long long>(split_keys) * (HD / 4);
+  if (idx >= per_gh * B * Hkv) return;
+  const int gh = static_cast<int>(idx / per_gh);
+  const int rem = static_cast<int>(idx % per_gh);
+  const int key = rem / (HD / 4), d = 4 * (rem % (HD / 4));
+  const size_t plane = static_cast<size_t>(B) * Hkv * S * HD;
+  const size_t src = (static_cast<size_t>(gh) * S + key) * HD + d;
+  const f32x4 k0 = *reinterpret_cast<const f32x4*>(part + src);
+  const f32x4 v0 = *reinterpret_cast<const f32x4*>(part + plane + src);
+  const f32x4 k1 = *reinterpret_cast<const f32x4*>(part + 2 * plane + src);
+  const f32x4 v1 = *reinterpret_cast<const f32x4*>(part + 3 * plane + src);
+  const int b = gh / Hkv, hkv = gh % Hkv;
+  const size_t dst = ((static_cast<size_t>(b) * S + key) * Hkv + hkv) * HD + d;
+  u16x4 ko, vo;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ko[j] = f2bf((k0[j] + k1[j]) * scale);
+    vo[j] = f2bf(v0[j] + v1[j]);
+  }
+  *reinterpret_cast<u16x4*>(dk + dst) = ko;
+  *reinterpret_cast<u16x4*>(dv + dst) = vo;
 }
 
 // dQ: one workgroup = 128 query rows of one (b, head); wave = 32 rows (the
@@ -725,8 +799,95 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// dK/dV job plan (host).  Causal key blocks carry very different work: block
+// kb sweeps G x (nqt - 4 kb) query tiles, so at S = 4096 the first block does
+// 32x the last.  One workgroup per block left ~half the CU slots idle at the
+// end (fa_bwd_dkdv ran at ~22 % MFMA busy, profiles/r01_attn_counters): the
+// plan splits every block heavier than the average slot load into two halves
+// (fp32 partials, summed by fa_bwd_dkdv_finalize) and orders each XCD's jobs
+// longest-first (LPT), with all blocks of one (batch, kv head) on one XCD so
+// they share its L2 copy of Q / dO.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct BwdPlan {
+  int4* jobs = nullptr;  // device, grid entries
+  int grid = 0;
+  int split_keys = 0;    // keys [0, split_keys) of every (b, hkv) are split
+};
+
+BwdPlan make_plan(int B, int S, int Hq, int Hkv, int causal, int num_cus) {
+  BwdPlan p;
+  const int G = Hq / Hkv, nqt = (S + BQT - 1) / BQT, nKB = (S + 127) / 128;
+  const int groups = B * Hkv;
+  auto work = [&](int kb) { return G * (nqt - (causal ? (kb * 128) / BQT : 0)); };
+  double total = 0;
+  for (int kb = 0; kb < nKB; ++kb) total += static_cast<double>(work(kb)) * groups;
+  const double avg = total / (2.0 * num_cus);  // two dK/dV workgroups per CU
+  struct J { int4 j; int w; };
+  std::vector<std::vector<J>> per_xcd(8);
+  int nsplit = 0;
+  for (int kb = 0; kb < nKB; ++kb) {
+    const int w = work(kb);
+    const bool split = causal && w > avg && w >= 2 * G;
+    if (split) nsplit = kb + 1;
+    for (int gid = 0; gid < groups; ++gid) {
+      auto& L = per_xcd[gid % 8];
+      if (split) {
+        const int h = w / 2;
+        L.push_back({make_int4(gid, kb | (1 << 24), 0, h), h});
+        L.push_back({make_int4(gid, kb | (2 << 24), h, w), w - h});
+      } else {
+        L.push_back({make_int4(gid, kb, 0, w), w});
+      }
+    }
+  }
+  size_t len = 0;
+  for (auto& L : per_xcd) {
+    std::stable_sort(L.begin(), L.end(), [](const J& a, const J& b) { return a.w > b.w; });
+    len = std::max(len, L.size());
+  }
+  std::vector<int4> table(8 * len, make_int4(0, 0, 0, 0));  // padding: empty range
+  for (size_t i = 0; i < table.size(); ++i) {
+    const auto& L = per_xcd[i % 8];  // workgroup i is dispatched to XCD i % 8
+    if (i / 8 < L.size()) table[i] = L[i / 8].j;
+  }
+  if (hipMalloc(&p.jobs, table.size() * sizeof(int4)) != hipSuccess) return BwdPlan{};
+  if (hipMemcpy(p.jobs, table.data(), table.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(p.jobs);
+    return BwdPlan{};
+  }
+  p.grid = static_cast<int>(table.size());
+  p.split_keys = std::min(S, nsplit * 128);
+  return p;
+}
+
+// One plan per (device, shape), built on first use outside stream capture.
+const BwdPlan* get_plan(int B, int S, int Hq, int Hkv, int causal, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::array<int, 6>, BwdPlan> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const std::array<int, 6> key{dev, B, S, Hq, Hkv, causal};
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second.jobs ? &it->second : nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  BwdPlan p = make_plan(B, S, Hq, Hkv, causal, cus);
+  auto& slot = cache[key] = p;
+  return slot.jobs ? &slot : nullptr;
+}
+
+}  // namespace
+
 KGWE_API int64_t kgwe_flash_attn_bwd_workspace(int B, int S, int Hq, int Hkv, int D) {
-  return static_cast<int64_t>(B) * Hq * S * sizeof(float);  // delta
+  // delta, then the dK/dV halves' fp32 partials [2 halves][dk|dv][B][Hkv][S][D]
+  return static_cast<int64_t>(B) * Hq * S * sizeof(float) +
+         static_cast<int64_t>(4) * B * Hkv * S * HD * sizeof(float);
 }
 
 // lse2 from the forward (log2 units).  `work` >= workspace bytes.
@@ -745,25 +906,39 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
   const int nQB = (S + BQ - 1) / BQ;
   const bf16_t *Q = static_cast<const bf16_t*>(q), *Kp = static_cast<const bf16_t*>(k),
                *V = static_cast<const bf16_t*>(v), *DO = static_cast<const bf16_t*>(dout);
+  // Planned dK/dV jobs (balanced causal sweep); the analytic one-block-per-
+  // workgroup grid when no plan can be built (first call inside a capture).
+  const BwdPlan* plan = get_plan(B, S, Hq, Hkv, causal, s);
+  float* part = work + static_cast<size_t>(B) * Hq * S;
+  const int4* jobs = plan ? plan->jobs : nullptr;
+  const unsigned dkdv_grid = plan ? static_cast<unsigned>(plan->grid) : static_cast<unsigned>(B * Hkv * nKB);
   // EVEN: every tile is full (no per-row bounds checks in the inner loops).
   if (S % 256 == 0) {
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, dim3(static_cast<unsigned>(B * Hkv * nKB)), dim3(256), 0,
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, dim3(dkdv_grid), dim3(256), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
-                       S, Hq, Hkv, c, scale, causal, nKB);
+                       S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
     rc = KGWE_CHECK_LAUNCH();
     if (rc) return rc;
     hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
                        Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
                        nQB);
   } else {
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(static_cast<unsigned>(B * Hkv * nKB)), dim3(256), 0,
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(dkdv_grid), dim3(256), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
-                       S, Hq, Hkv, c, scale, causal, nKB);
+                       S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
     rc = KGWE_CHECK_LAUNCH();
     if (rc) return rc;
     hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
                        Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
                        nQB);
+  }
+  rc = KGWE_CHECK_LAUNCH();
+  if (rc) return rc;
+  if (plan && plan->split_keys > 0) {
+    const long long n = static_cast<long long>(B) * Hkv * plan->split_keys * (HD / 4);
+    hipLaunchKernelGGL(fa_bwd_dkdv_finalize, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s,
+                       part, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv), B, S, Hkv, plan->split_keys,
+                       scale);
   }
   return KGWE_CHECK_LAUNCH();
 }

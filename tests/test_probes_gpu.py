@@ -7,11 +7,16 @@ pytestmark = pytest.mark.gpu
 def test_hbm_probe_reasonable():
     from kgwe.agent import probes
 
-    r = probes.probe_hbm(0, 1 << 30, 5)
-    # MI355X: 8 TB/s spec, ~6.3 TB/s achievable copy (MI355X_MICROARCH.md)
-    assert 2000 < r.copy_gbps < 8500, r
-    assert 2000 < r.read_gbps < 8500, r
-    assert 1000 < r.lds_copy_gbps < 8500, r
+    r = probes.probe_hbm(0, 1 << 30, 10)
+    # MI355X: 8 TB/s spec, 6.29 TB/s achievable float4 copy (MI355X_MICROARCH.md).
+    # Measured on this pool: copy 5.79, read 6.63, write 4.91 TB/s at 1 GiB
+    # (4 U-vector nontemporal streams per thread).  The node agent's
+    # degradation rule compares against this copy rate, so it must sit within
+    # ~15 % of the achievable number, not merely "above 2 TB/s".
+    assert 5300 < r.copy_gbps < 8000, r
+    assert 5800 < r.read_gbps < 8000, r
+    assert 4000 < r.write_gbps < 8000, r
+    assert 3500 < r.lds_copy_gbps < 8000, r
 
 
 @pytest.mark.multigpu

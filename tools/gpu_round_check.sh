@@ -3,6 +3,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+timeout -k 10 120 python -c "
+from kgwe.agent import probes
+for gb in (1, 4):
+    print(gb, 'GiB', probes.probe_hbm(0, gb << 30, 10))" > gpurun_out/probe_hbm.log 2>&1 || { tail -20 gpurun_out/probe_hbm.log; exit 1; }
+cat gpurun_out/probe_hbm.log
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -rs --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -5 gpurun_out/pytest_gpu.log
