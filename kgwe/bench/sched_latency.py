@@ -46,6 +46,7 @@ import multiprocessing as mp
 import os
 import queue
 import random
+import sys
 import threading
 import time
 
@@ -113,6 +114,7 @@ def full_node(name: str, i: int, gpus: int = 8) -> dict:
 def _apiserver_proc(conn):
     from ..controller.apiserver import FakeApiServer
 
+    sys.setswitchinterval(0.0005)  # threaded stand-in for a Go apiserver
     api = FakeApiServer().start()
     conn.send(api.url)
     while conn.recv() != "stop":  # "freeze": the fleet is loaded
@@ -131,6 +133,10 @@ def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev, ready_ev, node
     def on_preempted(victims):
         bound_q.put(("__preempted__", json.dumps(victims), 0.0, False))
 
+    # The stand-in is a threaded CPython process (watch, cycle, informer, 4
+    # binders): hand the GIL over at 0.5 ms instead of 5 ms, so the cycle
+    # thread is not parked behind a binder's JSON work (Go has no such lock).
+    sys.setswitchinterval(0.0005)
     # static fleet: the node list is cached like kube-scheduler's informer
     sim = SchedulerSim(KubeClient(api_url), ext_url, on_bound=on_bound, on_preempted=on_preempted,
                        node_cache_capable=node_cache, node_refresh_s=60.0).start()
@@ -152,6 +158,7 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
     from ..core import Platform, make_fixture
     from ..extender.server import ExtenderServer
 
+    sys.setswitchinterval(0.001)  # as kgwe.controller.main sets it for the extender's threads
     kube = KubeClient(api_url)
     # Housekeeping as the controller runs it (tick: gang expiry, cost sampling,
     # idle-partition reclaim).  Pod lifetimes here are seconds, not hours, so

@@ -12,6 +12,7 @@ from __future__ import annotations
 import argparse
 import json
 import signal
+import sys
 import threading
 import time
 
@@ -137,6 +138,11 @@ def main(argv=None) -> int:
     ap.add_argument("--set", action="append", default=[], help="override key.path=value")
     a = ap.parse_args(argv)
     cfg = load_config(DEFAULTS, a.config, a.set, env_prefix="KGWE_CONTROLLER_")
+    # The extender's verbs run in HTTP handler threads next to the reconciler:
+    # every C++ call releases the GIL, so hand it back at 1 ms (not CPython's
+    # 5 ms) and a verb waiting to re-enter Python is not parked behind a
+    # reconcile pass (profiles/r02_sched).
+    sys.setswitchinterval(0.001)
     plat, ext, rec = build(cfg)
     wh = cfg["webhook"]
     if wh["certFile"]:

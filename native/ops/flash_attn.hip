@@ -46,6 +46,7 @@
 #include <array>
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 using namespace kgwe;
@@ -77,11 +78,19 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ bf16x8 cat44(u16x4 lo, u16x4 hi) {
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);  // a register-pair concat
 }
+
+// Two floats -> one packed bf16 pair (RNE), ONE v_cvt_pk_bf16_f32.  Building
+// MFMA operands element-wise from f2bf() cost a convert per element plus
+// v_perm / v_or / v_mov to pack the halves (3x the VALU).
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+__device__ __forceinline__ unsigned pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
+}
+__device__ __forceinline__ bf16x8 pk8(const u32x4& w) { return __builtin_bit_cast(bf16x8, w); }
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
 // Accumulator register r of a 32x32 tile holds row (r&3) + 8*(r>>2) + 4*half.
 __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
         }
       }
       // P = 2^(S c - m): one FMA + one v_exp per element, then bf16 pairs.
-      bf16x8 pb[QPW][4];
+      u32x4 pb[QPW][4];
 #pragma unroll
       for (int j = 0; j < QPW; ++j) {
         float rs0 = 0.f, rs1 = 0.f;
@@ -315,8 +324,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
             const float p1 = fast_exp2(fmaf(sacc[j][st][r + 1], c, -m_use[j]));
             rs0 += p0;
             rs1 += p1;
-            pb[j][2 * st + (r >> 3)][r & 7] = f2bf(p0);
-            pb[j][2 * st + (r >> 3)][(r & 7) + 1] = f2bf(p1);
+            pb[j][2 * st + (r >> 3)][(r & 7) >> 1] = pk_bf16(p0, p1);
           }
         const float rs = rs0 + rs1;
         l[j] += rs + __shfl_xor(rs, 32, kWave);
@@ -336,7 +344,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
           const u16x4 hi = tr_read(Vc, voff[db][1] + rowc + 256 * 8);
           const bf16x8 vf = cat44(lo, hi);
 #pragma unroll
-          for (int j = 0; j < QPW; ++j) oacc[j][db] = mfma(vf, pb[j][s], oacc[j][db]);
+          for (int j = 0; j < QPW; ++j) oacc[j][db] = mfma(vf, pk8(pb[j][s]), oacc[j][db]);
         }
       }
     }
@@ -353,10 +361,10 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
       for (int db = 0; db < 4; ++db)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          u16x4 v4;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v4[jj] = f2bf(oacc[j][db][4 * g4 + jj] * inv);
-          *reinterpret_cast<u16x4*>(op + db * 32 + 8 * g4 + 4 * hh) = v4;
+          const f32x16& a = oacc[j][db];
+          const u32x2 v2 = {pk_bf16(a[4 * g4] * inv, a[4 * g4 + 1] * inv),
+                            pk_bf16(a[4 * g4 + 2] * inv, a[4 * g4 + 3] * inv)};
+          *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g4 + 4 * hh) = v2;
         }
       if (hh == 0)
         lse2[(static_cast<size_t>(b) * Hq + h) * S + qrow] = l[j] > 0.f ? m[j] + log2f(l[j]) : -INFINITY;
@@ -595,12 +603,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
       // dV^T += dO^T P ; dK^T += Q^T dS   (P, dS as B operands, permuted q order)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8 pb, sb;
+        u32x4 pw, sw;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pb[j] = f2bf(sa[8 * s + j]);
-          sb[j] = f2bf(pa[8 * s + j]);
+        for (int j = 0; j < 4; ++j) {
+          pw[j] = pk_bf16(sa[8 * s + 2 * j], sa[8 * s + 2 * j + 1]);
+          sw[j] = pk_bf16(pa[8 * s + 2 * j], pa[8 * s + 2 * j + 1]);
         }
+        const bf16x8 pb = pk8(pw), sb = pk8(sw);
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
           dva[db] = mfma(tr_rd(Dc, ao, 16 * s, db), pb, dva[db]);
@@ -638,14 +647,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        u16x4 a, bb;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[j] = f2bf(dka[db][4 * g4 + j] * scale);
-          bb[j] = f2bf(dva[db][4 * g4 + j]);
-        }
-        *reinterpret_cast<u16x4*>(dk + off + db * 32 + 8 * g4 + 4 * hh) = a;
-        *reinterpret_cast<u16x4*>(dv + off + db * 32 + 8 * g4 + 4 * hh) = bb;
+        const f32x16 &ka = dka[db], &va = dva[db];
+        const u32x2 a = {pk_bf16(ka[4 * g4] * scale, ka[4 * g4 + 1] * scale),
+                         pk_bf16(ka[4 * g4 + 2] * scale, ka[4 * g4 + 3] * scale)};
+        const u32x2 bb = {pk_bf16(va[4 * g4], va[4 * g4 + 1]), pk_bf16(va[4 * g4 + 2], va[4 * g4 + 3])};
+        *reinterpret_cast<u32x2*>(dk + off + db * 32 + 8 * g4 + 4 * hh) = a;
+        *reinterpret_cast<u32x2*>(dv + off + db * 32 + 8 * g4 + 4 * hh) = bb;
       }
   }
 }
@@ -759,21 +766,26 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           sa = mfma(row_rd(Kc, ao, st * 32, t), qf[t], sa);
           pa = mfma(row_rd(Vc, ao, st * 32, t), df[t], pa);
         }
+        auto softmax = [&](auto masked) {  // unmasked copy for full tiles (see dK/dV)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = fast_exp2(sa[r] * c - my_lse);
-          if (edge) {
-            const int kk = k0 + st * 32 + acc_row(r, hh);
-            if ((!EVEN && (kk >= S || qrow >= S)) || (causal && kk > qrow)) p = 0.f;
+          for (int r = 0; r < 16; ++r) {
+            float p = fast_exp2(sa[r] * c - my_lse);
+            if (decltype(masked)::value) {
+              const int kk = k0 + st * 32 + acc_row(r, hh);
+              if ((!EVEN && (kk >= S || qrow >= S)) || (causal && kk > qrow)) p = 0.f;
+            }
+            pa[r] = p * (pa[r] - my_delta);  // dS^T
           }
-          pa[r] = p * (pa[r] - my_delta);  // dS^T
-        }
+        };
+        if (edge) softmax(std::true_type{});
+        else softmax(std::false_type{});
         // dQ^T += K^T dS^T
 #pragma unroll
         for (int sp = 0; sp < 2; ++sp) {
-          bf16x8 sb;
+          u32x4 sw;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) sb[j] = f2bf(pa[8 * sp + j]);
+          for (int j = 0; j < 4; ++j) sw[j] = pk_bf16(pa[8 * sp + 2 * j], pa[8 * sp + 2 * j + 1]);
+          const bf16x8 sb = pk8(sw);
 #pragma unroll
           for (int db = 0; db < 4; ++db)
             dqa[db] = mfma(tr_rd(Kc, ao, st * 32 + 16 * sp, db), sb, dqa[db]);
@@ -789,10 +801,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        u16x4 a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = f2bf(dqa[db][4 * g4 + j] * scale);
-        *reinterpret_cast<u16x4*>(p + db * 32 + 8 * g4 + 4 * hh) = a;
+        const f32x16& qa = dqa[db];
+        const u32x2 a = {pk_bf16(qa[4 * g4] * scale, qa[4 * g4 + 1] * scale),
+                         pk_bf16(qa[4 * g4 + 2] * scale, qa[4 * g4 + 3] * scale)};
+        *reinterpret_cast<u32x2*>(p + db * 32 + 8 * g4 + 4 * hh) = a;
       }
   }
 }
@@ -819,9 +831,10 @@ struct BwdPlan {
 
 BwdPlan make_plan(int B, int S, int Hq, int Hkv, int causal, int num_cus) {
   BwdPlan p;
-  const int G = Hq / Hkv, nqt = (S + BQT - 1) / BQT, nKB = (S + 127) / 128;
+  constexpr int kblk = 128;  // keys per fa_bwd_dkdv_kernel workgroup
+  const int G = Hq / Hkv, nqt = (S + BQT - 1) / BQT, nKB = (S + kblk - 1) / kblk;
   const int groups = B * Hkv;
-  auto work = [&](int kb) { return G * (nqt - (causal ? (kb * 128) / BQT : 0)); };
+  auto work = [&](int kb) { return G * (nqt - (causal ? (kb * kblk) / BQT : 0)); };
   double total = 0;
   for (int kb = 0; kb < nKB; ++kb) total += static_cast<double>(work(kb)) * groups;
   const double avg = total / (2.0 * num_cus);  // two dK/dV workgroups per CU
@@ -859,7 +872,7 @@ BwdPlan make_plan(int B, int S, int Hq, int Hkv, int causal, int num_cus) {
     return BwdPlan{};
   }
   p.grid = static_cast<int>(table.size());
-  p.split_keys = std::min(S, nsplit * 128);
+  p.split_keys = std::min(S, nsplit * kblk);
   return p;
 }
 
@@ -908,7 +921,7 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
                *V = static_cast<const bf16_t*>(v), *DO = static_cast<const bf16_t*>(dout);
   // Planned dK/dV jobs (balanced causal sweep); the analytic one-block-per-
   // workgroup grid when no plan can be built (first call inside a capture).
-  const BwdPlan* plan = get_plan(B, S, Hq, Hkv, causal, s);
+  const BwdPlan* plan = get_plan(B, S, Hq, Hkv, causal, s);  // null: analytic grid
   float* part = work + static_cast<size_t>(B) * Hq * S;
   const int4* jobs = plan ? plan->jobs : nullptr;
   const unsigned dkdv_grid = plan ? static_cast<unsigned>(plan->grid) : static_cast<unsigned>(B * Hkv * nKB);
@@ -917,17 +930,18 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
     hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, dim3(dkdv_grid), dim3(256), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
                        S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
-    rc = KGWE_CHECK_LAUNCH();
-    if (rc) return rc;
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
-                       Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
-                       nQB);
   } else {
     hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(dkdv_grid), dim3(256), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
                        S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
-    rc = KGWE_CHECK_LAUNCH();
-    if (rc) return rc;
+  }
+  rc = KGWE_CHECK_LAUNCH();
+  if (rc) return rc;
+  if (S % 256 == 0) {
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
+                       Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
+                       nQB);
+  } else {
     hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
                        Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
                        nQB);

@@ -19,3 +19,8 @@ import csv,sys
 rows=list(csv.DictReader(open('$f')))
 for r in rows[:12]:
     print(r['Name'][:70].ljust(70), r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us', r['Percentage'][:5], '%')"
+rm -rf gpurun_out/fa_iter/pmc
+timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS \
+  -d gpurun_out/fa_iter/pmc -o run --output-format csv -- python3 tools/attn_bwd_only.py > gpurun_out/fa_iter/pmc.log 2>&1 || { tail -5 gpurun_out/fa_iter/pmc.log; exit 1; }
+f=$(find gpurun_out/fa_iter/pmc -name "*counter_collection.csv" | head -1)
+[ -n "$f" ] && python3 tools/pmc_dump.py "$f"
