@@ -200,6 +200,47 @@ static void test_metrics_exposition_labels() {
   CHECK(text.find("kgwe_test_gauge{node=\"n\\\"0\",gpu_uuid=\"GPU-1\"} 3") != std::string::npos);
 }
 
+// Copy-on-write snapshots: a publish shares every untouched node with the
+// previous snapshot, clones only what it writes, and readers holding the old
+// snapshot keep seeing the old node.
+static void test_nodemap_copy_on_write() {
+  ClusterTopology a;
+  a.nodes.set("n0", node_from_json(make_mi355x_node_fixture("n0", 8, 2)));
+  a.nodes.set("n1", node_from_json(make_mi355x_node_fixture("n1", 8, 2)));
+  ClusterTopology b(a);
+  CHECK(b.nodes.same("n0", a.nodes) && b.nodes.same("n1", a.nodes));
+  b.nodes.mut("n1").gpus[0].health.status = HealthStatus::Unhealthy;
+  CHECK(b.nodes.same("n0", a.nodes));
+  CHECK(!b.nodes.same("n1", a.nodes));
+  CHECK(a.nodes.at("n1").gpus[0].health.status == HealthStatus::Healthy);
+  CHECK(b.nodes.at("n1").gpus[0].health.status == HealthStatus::Unhealthy);
+  int seen = 0;
+  for (const auto& kv : b.nodes) seen += static_cast<int>(kv.second.gpus.size());
+  CHECK(seen == 16 && b.total_gpus() == 16);
+  CHECK(b.nodes.find("n0")->second.name == "n0" && b.nodes.find("nx") == b.nodes.end());
+  b.nodes.erase("n0");
+  CHECK(b.nodes.size() == 1 && a.nodes.size() == 2);
+}
+
+// Committed gauge families are shared snapshots: a scrape taken before a
+// commit keeps its view; set() after a commit thaws the family.
+static void test_metrics_commit_snapshot() {
+  MetricRegistry reg;
+  reg.declare("kgwe_g", MetricType::Gauge, "help", {"node"});
+  GaugeBatch b1;
+  b1.set("kgwe_g", {"a"}, 1.0);
+  b1.set("kgwe_g", {"b"}, 2.0);
+  reg.commit(std::move(b1));
+  CHECK(reg.value("kgwe_g", {"b"}) == 2.0);
+  GaugeBatch b2;
+  b2.set("kgwe_g", {"c"}, 3.0);
+  reg.commit(std::move(b2));
+  CHECK(reg.value("kgwe_g", {"a"}) == 0.0 && reg.value("kgwe_g", {"c"}) == 3.0);
+  reg.set("kgwe_g", {"d"}, 4.0);
+  CHECK(reg.value("kgwe_g", {"c"}) == 3.0 && reg.value("kgwe_g", {"d"}) == 4.0);
+  CHECK(reg.expose().find("kgwe_g{node=\"d\"} 4") != std::string::npos);
+}
+
 static void test_partition_binpack() {
   auto p = make_platform(1);
   std::set<std::string> gpus_used;
@@ -305,6 +346,8 @@ int main(int argc, char** argv) {
   test_cost_math();
   test_metrics_exposition_labels();
   test_partition_binpack();
+  test_nodemap_copy_on_write();
+  test_metrics_commit_snapshot();
   test_concurrent_ledger_stress(8, iters);
   if (g_failures) {
     std::fprintf(stderr, "%d check(s) failed\n", g_failures);
