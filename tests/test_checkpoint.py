@@ -116,3 +116,35 @@ def test_gpu_checkpoint_side_stream_roundtrip(tmp_path):
         d = (x - y).abs()
         assert d.mean().item() < 0.02 * lr * 5
         assert (d > 0.5 * lr).float().mean().item() < 0.01
+
+
+@pytest.mark.gpu
+def test_gpu_checkpoint_mid_training_holds_one_step(tmp_path):
+    """a checkpoint saved while training continues must hold
+    exactly the state of its step.  The D2H snapshot runs on a side stream
+    and the next steps' AdamW must wait for it (``dp.fence_writes``); the
+    step-2 file is compared with a device-side clone taken on the compute
+    stream right after step 2, while steps 3-5 run on."""
+    os.environ.pop("WORLD_SIZE", None)
+    os.environ.pop("RANK", None)
+    info = kdist.init(force_group=False)
+    assert info.device.type == "cuda"
+    cfg = TrainConfig(model="tiny", seq_len=128, micro_batch=2, parallel="zero",
+                      ckpt_dir=str(tmp_path), ckpt_every=2)
+    a = Trainer(cfg, info)
+    a.step()
+    a.step()  # global step 2: snapshot launched on a side stream
+    a.dp.wait_params()  # compute stream waits for step 2's updates (no host sync)
+    want = [(b.master.clone(), b.m.clone(), b.v.clone()) for b in a.dp.buckets]
+    for _ in range(3):  # steps 3-5 overwrite master / m / v
+        a.step()
+    a.ckpt.flush()
+    torch.cuda.synchronize()
+    payload = torch.load(tmp_path / "step-00000002" / "rank0-of-1.pt", weights_only=True)
+    assert payload["step"] == 2
+    for (m0, m1, v1), hb in zip(want, payload["buckets"]):
+        assert torch.equal(m0.cpu(), hb["master"])
+        assert torch.equal(m1.cpu(), hb["m"])
+        assert torch.equal(v1.cpu(), hb["v"])
+    # and the live state did move on
+    assert not torch.equal(want[0][0], a.dp.buckets[0].master)
