@@ -47,6 +47,16 @@ class Generator:
         self.lens = torch.zeros(batch, dtype=torch.int32, device=self.dev)
         self.graph = None
         self.filled = 0  # host-side count of cached positions (no device sync)
+        # Fused decode projections (native/ops/gemv.hip): RMSNorm + residual,
+        # SwiGLU and the greedy argmax ride inside the weight-streaming GEMVs.
+        import os  # noqa: PLC0415
+
+        self.fused = (self.dev.type == "cuda" and os.environ.get("KGWE_DECODE_FUSED", "1") != "0"
+                      and dec.gemv_supported(batch, c.dim) and dec.gemv_supported(batch, hq * d))
+        if self.fused:
+            self.hbuf = torch.empty(2, batch, c.dim, device=self.dev, dtype=p.dtype)
+            self.best = torch.zeros(batch, dec.argmax_slots(c.vocab_size), dtype=torch.long, device=self.dev)
+            self.w2_fused = dec.gemv_supported(batch, c.ffn_dim)
 
     # ------------------------------------------------------------ prefill
     @torch.no_grad()
@@ -87,7 +97,42 @@ class Generator:
 
     # ------------------------------------------------------------ decode
     @torch.no_grad()
+    def _step_fused(self) -> None:
+        """One decode step in 5 projection kernels per layer + RoPE/append +
+        attention: [RMSNorm(+res) -> wqkv], wo, [RMSNorm(+res) -> w13 -> SwiGLU],
+        w2, and [RMSNorm(+res) -> LM head -> argmax] at the end."""
+        c, m = self.cfg, self.m
+        hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
+        B, eps = self.B, c.norm_eps
+        x = m.tok_embeddings(self.tok)  # [B, dim]
+        res = None
+        hA, hB = self.hbuf[0], self.hbuf[1]
+        for i, layer in enumerate(m.layers):
+            at, ff = layer.attention, layer.feed_forward
+            if res is None:
+                qkv = dec.gemv(x, at.wqkv, dec.GEMV_NORM, g=layer.attention_norm, eps=eps)
+                h = x
+            else:
+                qkv = dec.gemv(x, at.wqkv, dec.GEMV_NORM, res=res, g=layer.attention_norm, eps=eps, h_out=hA)
+                h = hA
+            q = dec.rope_append(qkv, self.pos, self.cos, self.sin, self.kv[0, i], self.kv[1, i], hq, hkv, d)
+            o = self.attn(q, self.kv[0, i], self.kv[1, i], self.lens)
+            a = dec.gemv(o.view(B, -1), at.wo)
+            f = dec.gemv(a, ff.w13, dec.GEMV_NORM_SWIGLU, res=h, g=layer.ffn_norm, eps=eps, h_out=hB)
+            x = dec.gemv(f, ff.w2) if self.w2_fused else K.linear(f, ff.w2)
+            res = hB
+        if self.keep_logits and self.logits is None:
+            self.logits = torch.empty(B, c.vocab_size, device=self.dev, dtype=x.dtype)
+        dec.gemv(x, m.output, dec.GEMV_NORM_ARGMAX, res=res, g=m.norm, eps=eps,
+                 y=self.logits if self.keep_logits else None, best=self.best)
+        dec.argmax_finish(self.best, self.tok)
+        self.pos.add_(1)
+        self.lens.add_(1)
+
+    @torch.no_grad()
     def _step(self) -> None:
+        if self.fused:
+            return self._step_fused()
         c, m = self.cfg, self.m
         hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
         h = m.tok_embeddings(self.tok)  # [B, dim]

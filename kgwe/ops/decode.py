@@ -4,7 +4,10 @@
   append of k / v to the head-major KV cache, one kernel;
 * ``decode_attention`` — split-K GQA attention of one query token per
   sequence over the cache (HBM-bound; one workgroup per (sequence, kv head,
-  key chunk) serves all query heads of the group).
+  key chunk) serves all query heads of the group);
+* ``gemv`` — the decode step's projections (M <= 8 rows) as weight-streaming
+  skinny GEMMs (``native/ops/gemv.hip``) with the layer's RMSNorm (+ residual
+  add), SwiGLU and greedy argmax fused in.
 
 On a GPU the HIP kernels are mandatory; on CPU the fp32 references below run
 (also the numerics oracle of the GPU tests).
@@ -107,3 +110,92 @@ class DecodeAttention:
                                      self.B, self.hq, self.hkv, self.d, self.smax, self.splits,
                                      1.0 / math.sqrt(self.d), stream(q)), "decode_attn")
         return out
+
+
+# ------------------------------------------------------------------ projections
+GEMV_PLAIN, GEMV_NORM, GEMV_SWIGLU, GEMV_NORM_SWIGLU, GEMV_NORM_ARGMAX = 0, 1, 2, 3, 5
+GEMV_M = (1, 2, 4, 8)
+
+
+def gemv_supported(M: int, K: int) -> bool:
+    return M in GEMV_M and K % 8 == 0 and M * K * 2 <= 96 * 1024
+
+
+def _rows_per_wave(N: int) -> int:
+    # fill >= ~512 workgroups of 4 waves before packing several rows per wave
+    return 1 if N <= 4096 else (2 if N <= 16384 else 4)
+
+
+def gemv_reference(x, w, mode=GEMV_PLAIN, res=None, g=None, eps=1e-5):
+    """fp32 oracle of ``gemv``: returns (y, h) with the same roundings as the
+    unfused path (bf16 h = x + res, bf16 normalised x)."""
+    h = x
+    xin = x.float()
+    if mode & GEMV_NORM:
+        if res is not None:
+            h = (x.float() + res.float()).to(x.dtype)
+        hf = h.float()
+        rstd = torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)
+        xin = (hf * rstd * g.float()).to(x.dtype).float()
+    if mode & GEMV_SWIGLU:
+        F = w.shape[0] // 2
+        gt = xin @ w[:F].float().t()
+        up = xin @ w[F:].float().t()
+        y = (gt / (1 + torch.exp(-gt)) * up).to(x.dtype)
+    else:
+        y = (xin @ w.float().t()).to(x.dtype)
+    return y, h
+
+
+def argmax_slots(N: int) -> int:
+    """Entries per row of the ARGMAX partial-maximum buffer for an [N, K] head."""
+    R = _rows_per_wave(N)
+    return (N + 4 * R - 1) // (4 * R)
+
+
+def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=None, eps: float = 1e-5,
+         h_out=None, y=None, best=None):
+    """x [M, K] bf16, w [N, K] (SWIGLU: [2F, K]) -> y [M, N] (SWIGLU: [M, F]).
+    NORM modes: h_out (written: the new residual stream x + res) must not
+    alias x / res.  ARGMAX: ``best`` int64 [M, argmax_slots(N)] receives one
+    packed (value, index) maximum per workgroup; ``argmax_finish`` reduces it."""
+    if not use_hip(x):
+        yy, h = gemv_reference(x, w, mode, res, g, eps)
+        if h_out is not None and res is not None and mode & GEMV_NORM:
+            h_out.copy_(h)
+        if mode == GEMV_NORM_ARGMAX and best is not None:
+            best.zero_()
+            best[:, 0] = yy.float().argmax(-1)  # CPU: the token itself in slot 0
+        if y is not None:
+            y.copy_(yy)
+            return y
+        return yy
+    M, K = x.shape
+    N = w.shape[0] // 2 if mode & GEMV_SWIGLU else w.shape[0]
+    _require(x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()
+             and w.shape[1] == K and gemv_supported(M, K), "gemv: bf16 contiguous x [M<=8, K%8==0], w [N, K]")
+    _require(not (mode & GEMV_NORM) or (g is not None and g.numel() == K), "gemv: NORM needs g [K]")
+    _require(res is None or (res.shape == x.shape and res.is_contiguous()), "gemv: res must match x")
+    _require(h_out is None or (h_out.shape == x.shape and h_out.data_ptr() not in (
+        x.data_ptr(), res.data_ptr() if res is not None else -1)), "gemv: h_out must not alias x / res")
+    _require(mode != GEMV_NORM_ARGMAX or (best is not None and best.dtype == torch.long
+                                          and best.numel() == M * argmax_slots(N)),
+             "gemv: ARGMAX needs best int64 [M, argmax_slots(N)]")
+    if y is None and mode != GEMV_NORM_ARGMAX:
+        y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    check(lib().kgwe_decode_gemv(ptr(x), ptr(res) if res is not None else None,
+                                 ptr(g) if g is not None else None,
+                                 ptr(h_out) if h_out is not None else None, float(eps), ptr(w),
+                                 ptr(y) if y is not None else None,
+                                 ptr(best) if best is not None else None, M, N, K, mode,
+                                 _rows_per_wave(N), stream(x)), "decode_gemv")
+    return y
+
+
+def argmax_finish(best: torch.Tensor, tok: torch.Tensor) -> None:
+    """best [M, slots] (GEMV_NORM_ARGMAX partial maxima) -> tok [M] int64."""
+    if not use_hip(best):
+        tok.copy_(best[:, 0])
+        return
+    M, slots = best.shape
+    check(lib().kgwe_decode_argmax_finish(ptr(best), ptr(tok), M, slots, stream(best)), "decode_argmax_finish")

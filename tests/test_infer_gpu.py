@@ -57,6 +57,49 @@ def test_rope_append_matches_reference():
     assert torch.equal(vc.cpu(), vr)
 
 
+@pytest.mark.parametrize("M,N,K,mode", [
+    (1, 384, 2048, 0), (4, 3072, 2048, 1), (8, 520, 2048, 1), (4, 2048, 8192, 0),
+    (2, 1024, 2048, 3), (4, 4096, 2048, 3), (4, 20000, 2048, 1), (4, 96, 64, 2),
+])
+def test_gemv_modes_match_fp32_reference(M, N, K, mode):
+    from kgwe.ops import decode as dec
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).bfloat16()
+    res = (torch.randn(M, K, device="cuda", generator=g) * 0.5).bfloat16() if mode & dec.GEMV_NORM else None
+    rows = 2 * N if mode & dec.GEMV_SWIGLU else N
+    w = (torch.randn(rows, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    gw = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).bfloat16()
+    h_out = torch.empty_like(x) if res is not None else None
+    y = dec.gemv(x, w, mode, res=res, g=gw if mode & dec.GEMV_NORM else None, h_out=h_out)
+    torch.cuda.synchronize()
+    yr, hr = dec.gemv_reference(x.cpu(), w.cpu(), mode, res=None if res is None else res.cpu(),
+                                g=gw.cpu() if mode & dec.GEMV_NORM else None)
+    rel = (y.cpu().float() - yr.float()).norm() / yr.float().norm()
+    assert rel < 1e-2, rel.item()
+    if h_out is not None:
+        assert torch.equal(h_out.cpu(), hr)
+
+
+def test_gemv_argmax_matches_torch_argmax():
+    from kgwe.ops import decode as dec
+
+    g = torch.Generator(device="cuda").manual_seed(4)
+    M, N, K = 4, 50000, 2048
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    w[123] = w[77]  # an exact tie: the first index must win, as in torch.argmax
+    gw = torch.ones(K, device="cuda", dtype=torch.bfloat16)
+    best = torch.zeros(M, dec.argmax_slots(N), dtype=torch.long, device="cuda")
+    tok = torch.empty(M, dtype=torch.long, device="cuda")
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    for _ in range(2):  # a second step overwrites every partial
+        dec.gemv(x, w, dec.GEMV_NORM_ARGMAX, g=gw, y=y, best=best)
+        dec.argmax_finish(best, tok)
+        torch.cuda.synchronize()
+        assert torch.equal(tok, y.argmax(-1)), (tok, y.argmax(-1))
+
+
 @pytest.mark.parametrize("preset", ["tiny", "llama3.2-1b"])
 def test_graph_decode_logits_match_full_forward(preset):
     from kgwe.models import llama
@@ -66,6 +109,7 @@ def test_graph_decode_logits_match_full_forward(preset):
     m = llama.build(preset, device="cuda", dtype=torch.bfloat16)
     m.eval()
     gen = Generator(m, batch=2, max_seq=96, keep_logits=True)
+    assert gen.fused  # the fused GEMV decode path is the one under test
     prompt = torch.randint(0, m.cfg.vocab_size, (2, 40), device="cuda")
     gen.prefill(prompt)
     gen.capture()
