@@ -53,9 +53,9 @@ _SIGS = {
     "kgwe_decode_attn_workspace": (c_int64, [c_int, c_int, c_int, c_int]),
     "kgwe_decode_attn_splits": (c_int, [c_int, c_int, c_int]),
     "kgwe_decode_gemv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
-                                 c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+                                 c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "kgwe_decode_argmax_finish": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
-    "kgwe_decode_argmax_slots": (c_int, [c_int, c_int]),
+    "kgwe_decode_argmax_slots": (c_int, [c_int, c_int, c_int]),
     "kgwe_adamw_tensor_bytes": (c_int, []),
 }
 _OPTIONAL_SIGS = {

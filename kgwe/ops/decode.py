@@ -147,10 +147,36 @@ def gemv_reference(x, w, mode=GEMV_PLAIN, res=None, g=None, eps=1e-5):
     return y, h
 
 
+_MAX_WGS = None
+
+
+def max_wgs() -> int:
+    """Grid cap of the decode GEMVs: 8 workgroups per CU this process may use
+    (a CoLocate share's ``KGWE_CU_RANGE`` = "begin-end", else the device)."""
+    global _MAX_WGS
+    if _MAX_WGS is None:
+        import os  # noqa: PLC0415
+
+        cus = 0
+        rng = os.environ.get("KGWE_CU_RANGE", "")
+        if "-" in rng:
+            try:
+                b, e = (int(v) for v in rng.split("-"))
+                cus = max(0, e - b)
+            except ValueError:
+                cus = 0
+        if cus <= 0:
+            cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+                if torch.cuda.is_available() else 256
+        _MAX_WGS = 8 * cus
+    return _MAX_WGS
+
+
 def argmax_slots(N: int) -> int:
-    """Entries per row of the ARGMAX partial-maximum buffer for an [N, K] head."""
+    """Entries per row of the ARGMAX partial-maximum buffer for an [N, K] head
+    (one per workgroup of the capped grid)."""
     R = _rows_per_wave(N)
-    return (N + 4 * R - 1) // (4 * R)
+    return min((N + 4 * R - 1) // (4 * R), max_wgs())
 
 
 def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=None, eps: float = 1e-5,
@@ -188,7 +214,7 @@ def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=N
                                  ptr(h_out) if h_out is not None else None, float(eps), ptr(w),
                                  ptr(y) if y is not None else None,
                                  ptr(best) if best is not None else None, M, N, K, mode,
-                                 _rows_per_wave(N), stream(x)), "decode_gemv")
+                                 _rows_per_wave(N), max_wgs(), stream(x)), "decode_gemv")
     return y
 
 

@@ -20,6 +20,8 @@
 //            greedy token needs no separate argmax over the vocabulary.
 //
 // Every kernel here is graph-safe (no host sync, fixed grids).
+#include <algorithm>
+
 #include "common.h"
 
 using namespace kgwe;
@@ -129,8 +131,14 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane / L, li = lane % L;
-  const int n = (blockIdx.x * 4 + w) * R + r;  // output column of this lane group
-  const bool valid = n < N;
+  // Workgroups loop over blocks of 4 R columns (grid capped at a few per
+  // visible CU): the staging below is paid once per workgroup, not once per
+  // block — under a CoLocate CU mask (32 CUs) an uncapped grid repeated it
+  // 8x as often per CU and ran slower than hipBLASLt.
+  const int nblk = (N + 4 * R - 1) / (4 * R);
+  int blk = blockIdx.x;
+  int n = (blk * 4 + w) * R + r;  // output column of this lane group
+  bool valid = n < N;
   const bf16_t* wg = W + static_cast<size_t>(valid ? n : 0) * K;
   const bf16_t* wu = SWIGLU ? W + static_cast<size_t>(valid ? N + n : 0) * K : nullptr;
   const int stride = 8 * L;  // elements per lane-group pass
@@ -138,7 +146,6 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(
   // staged, so their HBM latency overlaps the staging (at K <= 8 * L *
   // UNROLL that is the whole row: decode projections are latency-bound).
   bf16x8 wv[UNROLL], uv[SWIGLU ? UNROLL : 1];
-  int k = 8 * li;
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -147,52 +154,70 @@ __global__ __launch_bounds__(kThreads) void gemv_kernel(
       if (SWIGLU) uv[u] = in ? *reinterpret_cast<const bf16x8*>(wu + k0 + u * stride) : bf16x8{};
     }
   };
-  fetch(k);
-  // PLAIN/SWIGLU read x straight from global memory (every wave of the CU
-  // reads the same few KB: L1 hits) — no staging pass, no barrier.  The NORM
-  // modes need the whole row's RMS first, so they normalise into LDS.
-  if (NORM) stage_x<NORM>(xs, x, res, g, h_out, eps, M, K, red);
-  const bf16_t* xsrc = NORM ? xs : x;
+  fetch(8 * li);
+  // x is staged in LDS in every mode: read from global memory inside the dot
+  // loop, each x load's vmcnt wait also drained the weight loads in flight
+  // (one counter), serialising the stream.  LDS reads wait on lgkmcnt.
+  stage_x<NORM>(xs, x, res, g, h_out, eps, M, K, red);
+  const bf16_t* xsrc = xs;
+  unsigned long long run[ARGMAX ? M : 1];
+#pragma unroll
+  for (int m = 0; m < (ARGMAX ? M : 1); ++m) run[m] = 0ull;
 
-  float acc[M], accu[SWIGLU ? M : 1];
+  for (; blk < nblk; blk += gridDim.x) {
+    float acc[M], accu[SWIGLU ? M : 1];
 #pragma unroll
-  for (int m = 0; m < M; ++m) acc[m] = 0.f;
-  if (SWIGLU)
+    for (int m = 0; m < M; ++m) acc[m] = 0.f;
+    if (SWIGLU)
 #pragma unroll
-    for (int m = 0; m < M; ++m) accu[m] = 0.f;
-  for (; k < K; k += UNROLL * stride) {
+      for (int m = 0; m < M; ++m) accu[m] = 0.f;
+    for (int k = 8 * li; k < K; k += UNROLL * stride) {
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      if (k + u * stride >= K) break;  // lane-group uniform
+      for (int u = 0; u < UNROLL; ++u) {
+        if (k + u * stride >= K) break;  // lane-group uniform
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xsrc + static_cast<size_t>(m) * K + k + u * stride);
-        acc[m] = dot8(wv[u], xv, acc[m]);
-        if (SWIGLU) accu[m] = dot8(uv[SWIGLU ? u : 0], xv, accu[m]);
+        for (int m = 0; m < M; ++m) {
+          const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xsrc + static_cast<size_t>(m) * K + k + u * stride);
+          acc[m] = dot8(wv[u], xv, acc[m]);
+          if (SWIGLU) accu[m] = dot8(uv[SWIGLU ? u : 0], xv, accu[m]);
+        }
+      }
+      if (k + UNROLL * stride < K) fetch(k + UNROLL * stride);
+    }
+    const int n_done = n;
+    const bool valid_done = valid;
+    const int nb = blk + gridDim.x;  // prefetch the next block's rows now
+    if (nb < nblk) {
+      n = (nb * 4 + w) * R + r;
+      valid = n < N;
+      wg = W + static_cast<size_t>(valid ? n : 0) * K;
+      if (SWIGLU) wu = W + static_cast<size_t>(valid ? N + n : 0) * K;
+      fetch(8 * li);
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      acc[m] = group_sum<L>(acc[m]);
+      if (SWIGLU) accu[m] = group_sum<L>(accu[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float v = acc[m];
+      if (SWIGLU) v = v / (1.f + __expf(-v)) * accu[m];
+      const bf16_t o = f2bf(v);
+      if (y && valid_done && li == 0) y[static_cast<size_t>(m) * N + n_done] = o;
+      if (ARGMAX && valid_done) {
+        const unsigned long long key = argmax_key(bf2f(o), n_done);
+        run[ARGMAX ? m : 0] = key > run[ARGMAX ? m : 0] ? key : run[ARGMAX ? m : 0];
       }
     }
-    if (k + UNROLL * stride < K) fetch(k + UNROLL * stride);
-  }
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    acc[m] = group_sum<L>(acc[m]);
-    if (SWIGLU) accu[m] = group_sum<L>(accu[m]);
-  }
-  float out[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    float v = acc[m];
-    if (SWIGLU) v = v / (1.f + __expf(-v)) * accu[m];
-    out[m] = bf2f(f2bf(v));
-    if (y && valid && li == 0) y[static_cast<size_t>(m) * N + n] = f2bf(v);
   }
   if (ARGMAX) {
-    // Workgroup argmax of its 4 R columns per row, ONE partial per workgroup
-    // (best[m * gridDim.x + block]); argmax_finish reduces the partials.
+    // Workgroup argmax over every column it produced, ONE partial per
+    // workgroup (best[m * gridDim.x + block]); argmax_finish reduces them.
     // (A global atomicMax per column serialised 500k atomics on M words.)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      unsigned long long key = valid ? argmax_key(out[m], n) : 0ull;
+      unsigned long long key = run[ARGMAX ? m : 0];
 #pragma unroll
       for (int off = L; off < kWave; off <<= 1) {
         const unsigned long long o = __shfl_xor(key, off, kWave);
@@ -227,10 +252,11 @@ int launch_one(const dim3& grid, size_t lds, const bf16_t* x, const bf16_t* res,
 
 template <int R, int M>
 int launch_m(int mode, const void* x, const void* res, const void* g, void* h_out, float eps,
-             const void* W, void* y, unsigned long long* best, int N, int K, hipStream_t s) {
+             const void* W, void* y, unsigned long long* best, int N, int K, int max_wgs, hipStream_t s) {
   const int rows_per_wg = 4 * R;
-  const dim3 grid((N + rows_per_wg - 1) / rows_per_wg);
-  const size_t lds = (mode & kNorm) ? static_cast<size_t>(M) * K * sizeof(bf16_t) : 0;
+  const int nblk = (N + rows_per_wg - 1) / rows_per_wg;
+  const dim3 grid(max_wgs > 0 ? std::min(nblk, max_wgs) : nblk);
+  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t);
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(res);
   auto G = static_cast<const bf16_t*>(g);
@@ -249,12 +275,12 @@ int launch_m(int mode, const void* x, const void* res, const void* g, void* h_ou
 
 template <int R>
 int launch_r(int M, int mode, const void* x, const void* res, const void* g, void* h_out, float eps,
-             const void* W, void* y, unsigned long long* best, int N, int K, hipStream_t s) {
+             const void* W, void* y, unsigned long long* best, int N, int K, int max_wgs, hipStream_t s) {
   switch (M) {
-    case 1: return launch_m<R, 1>(mode, x, res, g, h_out, eps, W, y, best, N, K, s);
-    case 2: return launch_m<R, 2>(mode, x, res, g, h_out, eps, W, y, best, N, K, s);
-    case 4: return launch_m<R, 4>(mode, x, res, g, h_out, eps, W, y, best, N, K, s);
-    case 8: return launch_m<R, 8>(mode, x, res, g, h_out, eps, W, y, best, N, K, s);
+    case 1: return launch_m<R, 1>(mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
+    case 2: return launch_m<R, 2>(mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
+    case 4: return launch_m<R, 4>(mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
+    case 8: return launch_m<R, 8>(mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
     default: return -1;
   }
 }
@@ -299,23 +325,25 @@ __global__ __launch_bounds__(kFinishThreads) void argmax_finish_kernel(
 // best [M * kgwe_decode_argmax_slots(N, rows_per_wave)] u64: one partial
 // maximum per workgroup, reduced by kgwe_decode_argmax_finish.
 // rows_per_wave: 1, 2 or 4 (more rows per wave = fewer lanes per row).
+// max_wgs > 0 caps the grid (workgroups then loop over column blocks).
 KGWE_API int kgwe_decode_gemv(const void* x, const void* res, const void* g, void* h_out, float eps,
                               const void* W, void* y, unsigned long long* best, int M, int N, int K,
-                              int mode, int rows_per_wave, hipStream_t s) {
+                              int mode, int rows_per_wave, int max_wgs, hipStream_t s) {
   if (K % 8 || N <= 0 || K <= 0 || M <= 0 || M > kMaxM) return -1;
   if (static_cast<size_t>(M) * K * sizeof(bf16_t) > 96 * 1024) return -1;  // LDS staging bound
   if ((mode & kNorm) && !g) return -1;
   if (mode == kNormArgmax && !best) return -1;
   switch (rows_per_wave) {
-    case 1: return launch_r<1>(M, mode, x, res, g, h_out, eps, W, y, best, N, K, s);
-    case 2: return launch_r<2>(M, mode, x, res, g, h_out, eps, W, y, best, N, K, s);
-    case 4: return launch_r<4>(M, mode, x, res, g, h_out, eps, W, y, best, N, K, s);
+    case 1: return launch_r<1>(M, mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
+    case 2: return launch_r<2>(M, mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
+    case 4: return launch_r<4>(M, mode, x, res, g, h_out, eps, W, y, best, N, K, max_wgs, s);
     default: return -1;
   }
 }
 
-KGWE_API int kgwe_decode_argmax_slots(int N, int rows_per_wave) {
-  return (N + 4 * rows_per_wave - 1) / (4 * rows_per_wave);  // workgroups of the ARGMAX launch
+KGWE_API int kgwe_decode_argmax_slots(int N, int rows_per_wave, int max_wgs) {
+  const int nblk = (N + 4 * rows_per_wave - 1) / (4 * rows_per_wave);  // workgroups of the ARGMAX launch
+  return max_wgs > 0 ? std::min(nblk, max_wgs) : nblk;
 }
 
 KGWE_API int kgwe_decode_argmax_finish(const unsigned long long* best, long long* tok, int M, int slots,
