@@ -1,5 +1,7 @@
 #include "hal.h"
 
+#include <array>
+
 #include <dlfcn.h>
 
 #include <cstdio>
@@ -173,6 +175,9 @@ void FakeHal::set_health_signals(const std::string& gpu, const Json& j) {
   h.xgmi_links_down = static_cast<int>(j.get("xgmi_links_down").as_int(h.xgmi_links_down));
   h.retired_pages = j.get("retired_pages").as_int(h.retired_pages);
   h.pending_retired_pages = j.get("pending_retired_pages").as_int(h.pending_retired_pages);
+  h.cper_fatal = j.get("cper_fatal").as_int(h.cper_fatal);
+  h.cper_uncorrected = j.get("cper_uncorrected").as_int(h.cper_uncorrected);
+  h.cper_corrected = j.get("cper_corrected").as_int(h.cper_corrected);
   if (j.get("throttle").is_array()) {
     h.throttle_reasons.clear();
     for (const auto& t : j.get("throttle").items()) h.throttle_reasons.push_back(t.str());
@@ -234,9 +239,15 @@ struct AmdSmiHal::Impl {
   KGWE_SMI_FN(amdsmi_get_gpu_xgmi_link_status)
   KGWE_SMI_FN(amdsmi_get_gpu_bad_page_info)
   KGWE_SMI_FN(amdsmi_get_violation_status)
+  KGWE_SMI_FN(amdsmi_get_gpu_cper_entries)
 #undef KGWE_SMI_FN
   std::vector<amdsmi_processor_handle> handles;
   std::vector<std::string> uuids;
+  // CPER: per-GPU read cursor and cumulative counts by severity (the driver
+  // keeps a ring of records; the cursor walks it once).
+  std::vector<uint64_t> cper_cursor;
+  std::vector<std::array<int64_t, 3>> cper_counts;
+  std::vector<uint8_t> cper_primed;  // first read only advances the cursor past history
 };
 
 AmdSmiHal::AmdSmiHal() : impl_(new Impl) {
@@ -280,6 +291,7 @@ AmdSmiHal::AmdSmiHal() : impl_(new Impl) {
   KGWE_SMI_OPT(amdsmi_get_gpu_xgmi_link_status)
   KGWE_SMI_OPT(amdsmi_get_gpu_bad_page_info)
   KGWE_SMI_OPT(amdsmi_get_violation_status)
+  KGWE_SMI_OPT(amdsmi_get_gpu_cper_entries)
 #undef KGWE_SMI_OPT
   if (impl_->amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) {
     err_ = "amdsmi_init failed (no amdgpu driver?)";
@@ -308,6 +320,9 @@ AmdSmiHal::AmdSmiHal() : impl_(new Impl) {
     if (u.empty()) u = "GPU-amdsmi-" + std::to_string(i);
     impl_->uuids.push_back(u);
   }
+  impl_->cper_cursor.assign(impl_->handles.size(), 0);
+  impl_->cper_counts.assign(impl_->handles.size(), {0, 0, 0});
+  impl_->cper_primed.assign(impl_->handles.size(), 0);
   ok_ = true;
 }
 
@@ -476,6 +491,34 @@ void AmdSmiHal::refresh_telemetry(NodeTopology& n) {
         if (on(vs->active_vr_thrm)) g.health.throttle_reasons.push_back("vr_thermal");
         if (on(vs->active_hbm_thrm)) g.health.throttle_reasons.push_back("hbm_thermal");
       }
+    }
+    if (I.amdsmi_get_gpu_cper_entries) {
+      // New records since the last read (bounded: at most 8 x 64 per refresh).
+      constexpr uint32_t kMask = (1u << AMDSMI_CPER_SEV_NON_FATAL_UNCORRECTED) | (1u << AMDSMI_CPER_SEV_FATAL) |
+                                 (1u << AMDSMI_CPER_SEV_NON_FATAL_CORRECTED);
+      std::vector<char> data(64 * 1024);
+      std::vector<amdsmi_cper_hdr_t*> hdrs(64, nullptr);
+      auto& counts = I.cper_counts[g.index];
+      // Records cached before this agent started (an error the GPU was reset
+      // from, possibly days ago) are skipped: the first read only moves the
+      // cursor to the end of the ring.
+      const bool count_them = I.cper_primed[g.index] != 0;
+      for (int round = 0; round < (count_them ? 8 : 1024); ++round) {
+        uint64_t size = data.size(), count = hdrs.size();
+        const amdsmi_status_t st = I.amdsmi_get_gpu_cper_entries(h, kMask, data.data(), &size, hdrs.data(), &count,
+                                                                 &I.cper_cursor[g.index]);
+        if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_MORE_DATA) break;
+        for (uint64_t k = 0; k < count && k < hdrs.size(); ++k) {
+          if (!hdrs[k]) continue;
+          const int sev = static_cast<int>(hdrs[k]->error_severity);
+          if (count_them && sev >= 0 && sev < 3) ++counts[sev];
+        }
+        if (st != AMDSMI_STATUS_MORE_DATA || count == 0) break;
+      }
+      I.cper_primed[g.index] = 1;
+      g.health.cper_uncorrected = counts[AMDSMI_CPER_SEV_NON_FATAL_UNCORRECTED];
+      g.health.cper_fatal = counts[AMDSMI_CPER_SEV_FATAL];
+      g.health.cper_corrected = counts[AMDSMI_CPER_SEV_NON_FATAL_CORRECTED];
     }
     if (!g.health.pinned) {
       int down = 0;

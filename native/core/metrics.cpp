@@ -230,6 +230,8 @@ void MetricRegistry::declare_kgwe_families() {
           {"gpu_uuid", "node", "state"});
   declare("kgwe_gpu_xgmi_errors", M::Gauge, "xGMI error state (0 none, 1 error, 2 multiple)",
           {"gpu_uuid", "node"});
+  declare("kgwe_gpu_cper_records", M::Gauge, "CPER error records since the agent started, by severity",
+          {"gpu_uuid", "node", "severity"});
   declare("kgwe_gpu_throttle_active", M::Gauge, "Active throttle / violation reasons",
           {"gpu_uuid", "node", "reason"});
   // Partitions (MIG analogue)

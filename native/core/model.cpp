@@ -214,6 +214,9 @@ GpuDevice gpu_from_json(const Json& j, const std::string& node) {
   g.health.xgmi_links_down = static_cast<int>(h.get("xgmi_links_down").as_int(0));
   g.health.retired_pages = h.get("retired_pages").as_int(0);
   g.health.pending_retired_pages = h.get("pending_retired_pages").as_int(0);
+  g.health.cper_fatal = h.get("cper_fatal").as_int(0);
+  g.health.cper_uncorrected = h.get("cper_uncorrected").as_int(0);
+  g.health.cper_corrected = h.get("cper_corrected").as_int(0);
   for (const auto& r : h.get("throttle").items()) g.health.throttle_reasons.push_back(r.str());
   g.health.perf_degraded = h.get("perf_degraded").as_bool(false);
   g.health.perf_reason = h.get("perf_reason").str();
@@ -246,7 +249,11 @@ void apply_health_policy(Health& h, int links_down_in_topology) {
     degrade("correctable ECC storm (" + std::to_string(h.ecc_correctable) + ")");
   if (h.pending_retired_pages > 0)
     degrade(std::to_string(h.pending_retired_pages) + " HBM pages pending retirement");
+  if (h.cper_fatal > 0) fail(std::to_string(h.cper_fatal) + " fatal CPER error records");
   if (h.xgmi_errors > 0) degrade("xGMI errors reported");
+  if (h.cper_uncorrected > 0) degrade(std::to_string(h.cper_uncorrected) + " uncorrected (non-fatal) CPER records");
+  if (h.cper_corrected >= kCperCorrectedStorm)
+    degrade("corrected CPER storm (" + std::to_string(h.cper_corrected) + ")");
   if (h.perf_degraded) degrade(h.perf_reason.empty() ? "probe: degraded performance" : h.perf_reason);
   const int down = h.xgmi_links_down > links_down_in_topology ? h.xgmi_links_down : links_down_in_topology;
   // A down link is excluded per link by the group search; the GPU itself
@@ -327,6 +334,9 @@ Json to_json(const GpuDevice& g) {
   h["xgmi_links_down"] = g.health.xgmi_links_down;
   h["retired_pages"] = g.health.retired_pages;
   h["pending_retired_pages"] = g.health.pending_retired_pages;
+  h["cper_fatal"] = g.health.cper_fatal;
+  h["cper_uncorrected"] = g.health.cper_uncorrected;
+  h["cper_corrected"] = g.health.cper_corrected;
   h["pinned"] = g.health.pinned;
   h["perf_degraded"] = g.health.perf_degraded;
   h["perf_reason"] = g.health.perf_reason;

@@ -77,6 +77,11 @@ struct Health {
   int64_t retired_pages = 0;        // HBM pages retired (amdsmi_get_gpu_bad_page_info)
   int64_t pending_retired_pages = 0;  // marked bad, retired at the next reset
   std::vector<std::string> throttle_reasons;  // active violations: prochot, socket/vr/hbm thermal, ppt
+  // CPER (Common Platform Error Record) entries the driver cached for this
+  // GPU since the agent started (amdsmi_get_gpu_cper_entries), by severity.
+  int64_t cper_fatal = 0;
+  int64_t cper_uncorrected = 0;   // non-fatal uncorrected
+  int64_t cper_corrected = 0;     // non-fatal corrected
   // Measured-performance degradation reported by the node agent's probes
   // (e.g. HBM copy rate well below the node median).
   bool perf_degraded = false;
@@ -87,14 +92,17 @@ struct Health {
 // Health policy shared by every HAL backend (reference GPUHealth,
 // src/discovery/types.go:269-321; it only consumed `Healthy`).  Derives
 // status + reasons from the raw RAS / xGMI / throttle signals:
-//   Unhealthy: uncorrectable ECC, or retired pages >= kRetiredPageLimit
+//   Unhealthy: uncorrectable ECC, retired pages >= kRetiredPageLimit, or a
+//              FATAL CPER record
 //   Degraded : deferred ECC, correctable-ECC storm, pages pending retirement,
-//              xGMI errors, probe-measured performance degradation
+//              xGMI errors, non-fatal uncorrected CPER records, a corrected-
+//              CPER storm, probe-measured performance degradation
 //   reason only: xGMI links down (the group search drops the link, not the
 //              GPU) and active throttling (prochot, PPT power, socket / VR /
 //              HBM thermal — a GPU at full load routinely sits at its cap).
 constexpr int64_t kRetiredPageLimit = 64;
 constexpr int64_t kCorrectableStorm = 1000;
+constexpr int64_t kCperCorrectedStorm = 100;
 void apply_health_policy(Health& h, int links_down_in_topology = 0);
 
 // One schedulable slice of a partitioned GPU (CPX: 8 per GPU, one per XCD).

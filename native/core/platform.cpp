@@ -604,7 +604,8 @@ void Platform::refresh_gauges(double now_s) {
                         "kgwe_gpu_umc_activity_percent", "kgwe_gpu_memory_used_bytes",
                         "kgwe_gpu_memory_total_bytes", "kgwe_gpu_temperature_celsius", "kgwe_gpu_power_watts",
                         "kgwe_gpu_health_status", "kgwe_gpu_hbm_bandwidth_gbps", "kgwe_gpu_ecc_errors_total",
-                        "kgwe_gpu_retired_pages", "kgwe_gpu_xgmi_errors", "kgwe_gpu_throttle_active",
+                        "kgwe_gpu_retired_pages", "kgwe_gpu_xgmi_errors", "kgwe_gpu_cper_records",
+                        "kgwe_gpu_throttle_active",
                         "kgwe_gpu_partition_mode", "kgwe_partition_instance_count",
                         "kgwe_partition_instance_utilization_percent", "kgwe_xgmi_bandwidth_gbps",
                         "kgwe_xgmi_link_status", "kgwe_pcie_bandwidth_gbps", "kgwe_topology_score",
@@ -639,6 +640,10 @@ void Platform::refresh_gauges(double now_s) {
       batch.set("kgwe_gpu_retired_pages", {g.uuid, n.name, "pending"},
                 static_cast<double>(g.health.pending_retired_pages));
       batch.set("kgwe_gpu_xgmi_errors", {g.uuid, n.name}, static_cast<double>(g.health.xgmi_errors));
+      batch.set("kgwe_gpu_cper_records", {g.uuid, n.name, "fatal"}, static_cast<double>(g.health.cper_fatal));
+      batch.set("kgwe_gpu_cper_records", {g.uuid, n.name, "uncorrected"},
+                static_cast<double>(g.health.cper_uncorrected));
+      batch.set("kgwe_gpu_cper_records", {g.uuid, n.name, "corrected"}, static_cast<double>(g.health.cper_corrected));
       for (const auto& t : g.health.throttle_reasons) batch.set("kgwe_gpu_throttle_active", {g.uuid, n.name, t}, 1.0);
       batch.set("kgwe_gpu_partition_mode", {g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0);
       batch.set("kgwe_partition_instance_count", {g.uuid, n.name, to_string(g.partition.compute)},

@@ -23,12 +23,14 @@ def test_amdsmi_discovery_and_health_signals():
         assert g["partition"]["memory"] in ("NPS1", "NPS2")
         h = g["health"]
         for k in ("ecc_correctable", "ecc_uncorrectable", "ecc_deferred", "retired_pages",
-                  "pending_retired_pages", "xgmi_errors", "xgmi_links_down", "throttle"):
+                  "pending_retired_pages", "xgmi_errors", "xgmi_links_down", "throttle",
+                  "cper_fatal", "cper_uncorrected", "cper_corrected"):
             assert k in h, k
         assert h["status"] in ("Healthy", "Degraded", "Unhealthy")
         for k in ("ecc_correctable", "ecc_uncorrectable", "ecc_deferred", "retired_pages"):
             assert 0 <= h[k] < 2**40, (k, h[k])  # real counts, never uninitialised memory
-        assert (h["status"] == "Unhealthy") == (h["ecc_uncorrectable"] > 0 or h["retired_pages"] >= 64)
+        assert (h["status"] == "Unhealthy") == (h["ecc_uncorrectable"] > 0 or h["retired_pages"] >= 64
+                                                or h["cper_fatal"] > 0)
     # the scheduler places onto the real node
     p = Platform({})
     p.upsert_node(node)

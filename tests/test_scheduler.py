@@ -239,6 +239,10 @@ def test_topology_hints(plat):
     ({"xgmi_errors": 1}, "Degraded", "xGMI errors"),
     ({"xgmi_links_down": 1}, "Healthy", "link(s) down"),
     ({"throttle": ["hbm_thermal"]}, "Healthy", "throttling: hbm_thermal"),
+    ({"cper_fatal": 1}, "Unhealthy", "fatal CPER"),
+    ({"cper_uncorrected": 2}, "Degraded", "uncorrected (non-fatal) CPER"),
+    ({"cper_corrected": 150}, "Degraded", "corrected CPER storm"),
+    ({"cper_corrected": 3}, "Healthy", None),
 ])
 def test_health_policy_from_ras_signals(plat, signals, status, reason):
     """Fault injection through the fake amd-smi: raw RAS /
