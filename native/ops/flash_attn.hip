@@ -238,6 +238,15 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
   kwrite(0);
   gload(vb, 0);
   vwrite(0);
+  // Pin the Q loads before the loop.  Left alone, hipcc sinks them past the
+  // barrier to the loop entry, and the waitcnt pass — which cannot tell the
+  // first iteration from the rest — then waits vmcnt(7) .. vmcnt(0) at the
+  // eight S MFMAs of EVERY tile: the next tile's K prefetch is forced to land
+  // inside the first half of the S chain instead of under the whole tile.
+#pragma unroll
+  for (int j = 0; j < QPW; ++j)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(qf[j][t]));
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
@@ -558,6 +567,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     gload(g_cur, qt);
     swrite(0);
   }
+  // K fragments complete before the loop (see fa_fwd_kernel: otherwise the
+  // loop's first MFMAs wait for the prefetch issued just above them).
+#pragma unroll
+  for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(kf[t]));
   __syncthreads();
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
@@ -747,6 +760,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   const AOffs ao = make_aoffs(lane);
   gload(0);
   swrite(0);
+  // Q / dO fragments and row constants complete before the loop (see
+  // fa_fwd_kernel).
+#pragma unroll
+  for (int t = 0; t < 8; ++t) asm volatile("" ::"v"(qf[t]), "v"(df[t]));
+  asm volatile("" ::"v"(my_lse), "v"(my_delta));
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int cur = kt & 1;
@@ -961,10 +979,10 @@ KGWE_API int kgwe_flash_attn_fwd(const void* q, const void* k, const void* v, vo
                                  int B, int S, int Hq, int Hkv, int D, float scale, int causal,
                                  hipStream_t s) {
   if (D != HD || Hq % Hkv != 0 || B <= 0 || S <= 0) return -1;
+  const float c = scale * 1.4426950408889634f;  // softmax in the exp2 domain
   const int nQB = (S + BQF - 1) / BQF;
   const long long grid = static_cast<long long>(B) * Hq * nQB;
   if (grid > 0x7fffffff) return -1;
-  const float c = scale * 1.4426950408889634f;  // softmax in the exp2 domain
   if (S % 256 == 0)
     hipLaunchKernelGGL(fa_fwd_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(FNT), 0, s,
                        static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k),
