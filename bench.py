@@ -278,11 +278,20 @@ def rank_main(args) -> int:
         _release_memory()
         tc2 = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
                           activation_checkpointing=args.ckpt, parallel="fsdp")
-        tr2 = Trainer(tc2, info)
-        r2 = _row(tr2, timed_run(tr2, args.steps, min(args.warmup, 3)), args, info, kdist)
-        fsdp = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r2.items()
-                if k not in ("losses", "seconds")}
-        del tr2
+        # A secondary row: a failure on every rank alike (out of memory, an
+        # unsupported op) is reported in the row instead of losing the
+        # headline that was already measured.
+        try:
+            tr2 = Trainer(tc2, info)
+            r2 = _row(tr2, timed_run(tr2, args.steps, min(args.warmup, 3)), args, info, kdist)
+            fsdp = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r2.items()
+                    if k not in ("losses", "seconds")}
+            del tr2
+        except Exception as e:  # noqa: BLE001 - reported, never faked
+            print(f"[bench] rank {info.rank}: FSDP row failed: {e!r}", file=sys.stderr, flush=True)
+            fsdp = {"parallelism": f"fsdp{world}", "error": repr(e)[:300]}
+            tr2 = None
+            _release_memory()
     life.stop()
     life_util = [u[0] for u in kdist.all_gather_floats(
         [life.mean if life.mean is not None else -1.0], info)]
