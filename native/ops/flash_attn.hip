@@ -97,12 +97,31 @@ __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (
 
 // Decode a 1-D workgroup id into (b, hkv, g, qb): XCD-aware so consecutive
 // logical ids (same kv head) share an XCD; causal: heaviest query blocks first.
+//
+// Causal: each XCD holds a contiguous range of whole heads, and within it the
+// workgroups are dispatched heaviest query block FIRST ACROSS ALL its heads
+// (all last blocks, then all second-to-last, ...): longest-processing-time
+// order, so the last workgroups to start are the lightest.  Walking the
+// blocks of one head after another (heavy -> light, then the next head's
+// heavy block) put a 64-tile block at the end of every XCD's queue and left
+// ~25 % of the wave slots idle in the tail (SQ_WAVE_CYCLES vs GRBM_GUI_ACTIVE,
+// profiles/r02_attn).
 __device__ __forceinline__ void decode(int nQB, int G, int Hkv, bool causal, int* b, int* h,
                                        int* hkv, int* qb) {
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  int t = wg;
-  int q = t % nQB;
-  t /= nQB;
+  const int n = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, n);
+  int t, q;
+  const int per_xcd = n / 8;
+  if (causal && n % 8 == 0 && per_xcd % nQB == 0) {
+    const int heads = per_xcd / nQB;  // heads per XCD
+    const int xcd = wg / per_xcd, local = wg - xcd * per_xcd;
+    q = local / heads;
+    t = xcd * heads + local % heads;
+  } else {
+    t = wg;
+    q = t % nQB;
+    t /= nQB;
+  }
   const int g = t % G;
   t /= G;
   *hkv = t % Hkv;
