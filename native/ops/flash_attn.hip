@@ -13,8 +13,9 @@
 //     tile; O is rescaled only when some row's running max moved;
 //   * S^T = K Q^T is computed with the KEY on the accumulator rows and the
 //     query on the lane, so every lane owns one query row: the online-softmax
-//     row max / row sum are 32 in-lane ops + one cross-half exchange, and
-//     the O rescale is a per-lane scalar;
+//     row max is 32 in-lane ops + one v_permlane32_swap half exchange (the
+//     row sum's exchange waits for the epilogue), and the O rescale is a
+//     per-lane scalar;
 //   * the P accumulator is converted pairwise to bf16 and fed straight back
 //     as the B operand of O^T += V^T P (cdna_hip_programming.md §3
 //     "accumulator tile as the next MFMA's operand": the permuted k order
@@ -94,6 +95,17 @@ typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
 // Accumulator register r of a 32x32 tile holds row (r&3) + 8*(r>>2) + 4*half.
 __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+// max / sum of lane l and lane l ^ 32 in every lane: one v_permlane32_swap
+// (a VALU half exchange) instead of an LDS ds_bpermute round trip.
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 // Decode a 1-D workgroup id into (b, hkv, g, qb): XCD-aware so consecutive
 // logical ids (same kv head) share an XCD; causal: heaviest query blocks first.
@@ -220,11 +232,15 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
   // other (K loaded at the top and stored after the S MFMAs, V loaded then
   // and stored after the O MFMAs) to halve the staging registers.
   bf16x8 sr[NSTG];
+  // Addresses: a wave-uniform tile base plus a 32-bit per-lane offset (the
+  // global_load SGPR-base form), not a 64-bit multiply per chunk and tile.
+  const unsigned soff = static_cast<unsigned>(skey) * static_cast<unsigned>(kvs) + sch * 8u;
   auto gload = [&](const bf16_t* base, int kt) {
+    const bf16_t* tb = base + static_cast<size_t>(kt * BKV) * kvs;
 #pragma unroll
     for (int i = 0; i < NSTG; ++i) {
       const int s = kt * BKV + skey + 4 * FNW * i;
-      sr[i] = (EVEN || s < S) ? ld16(base + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
+      sr[i] = (EVEN || s < S) ? ld16(tb + (soff + static_cast<unsigned>(4 * FNW * i * kvs))) : bf16x8{};
     }
   };
   auto kwrite = [&](int buf) {
@@ -320,7 +336,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[j][st][r]);
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave)) * c;
+        mx = xhalf_max(mx) * c;
         const float m_new = fmaxf(m[j], mx);
         m_use[j] = m_new == -INFINITY ? 0.f : m_new;
         moved |= m_new > m[j];
@@ -355,7 +371,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
             pb[j][2 * st + (r >> 3)][(r & 7) >> 1] = pk_bf16(p0, p1);
           }
         const float rs = rs0 + rs1;
-        l[j] += rs + __shfl_xor(rs, 32, kWave);
+        l[j] += rs;  // this half-lane's 32 keys; the halves are summed once, at the end
       }
       // O^T += V^T P : P (key rows, query on lane) is the B operand as is; the
       // V^T fragment (d on the lane, the permuted key order of P on k) comes
@@ -382,8 +398,9 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
 #pragma unroll
   for (int j = 0; j < QPW; ++j) {
     const int qrow = q0 + 32 * j + lq;
+    const float lt = xhalf_sum(l[j]);
     if (EVEN || qrow < S) {
-      const float inv = l[j] > 0.f ? 1.f / l[j] : 0.f;
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
       bf16_t* op = o + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
       for (int db = 0; db < 4; ++db)
@@ -395,7 +412,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
           *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g4 + 4 * hh) = v2;
         }
       if (hh == 0)
-        lse2[(static_cast<size_t>(b) * Hq + h) * S + qrow] = l[j] > 0.f ? m[j] + log2f(l[j]) : -INFINITY;
+        lse2[(static_cast<size_t>(b) * Hq + h) * S + qrow] = lt > 0.f ? m[j] + log2f(lt) : -INFINITY;
     }
   }
 }
