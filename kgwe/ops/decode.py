@@ -96,7 +96,9 @@ class DecodeAttention:
                      "decode_attention: head_dim 64/128 and Hq/Hkv in {1,2,4,8}")
             self.splits = int(lib().kgwe_decode_attn_splits(B, hkv, smax))
             n = int(lib().kgwe_decode_attn_workspace(B, hq, d, self.splits))
-            self.work = torch.empty(n, device=device, dtype=torch.float32)
+            # zeroed once: the tail holds the split tickets, which every call
+            # returns to zero
+            self.work = torch.zeros(n, device=device, dtype=torch.float32)
 
     def __call__(self, q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, lens: torch.Tensor):
         if not self.hip:

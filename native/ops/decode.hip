@@ -12,7 +12,9 @@
 // Decode attention is HBM-bound (every cached K/V byte is read once per
 // step) and has little parallelism per sequence, so the key range of each
 // (sequence, kv-head) is split into `splits` chunks that run as separate
-// workgroups; a second kernel merges the partial softmax states.  One
+// workgroups; the LAST of them to finish merges the partial softmax states
+// in the same launch (write-through partials + one relaxed agent-scope
+// ticket per (sequence, kv-head): no fence, no spin, no second kernel).  One
 // workgroup serves ALL G = Hq/Hkv query heads of its kv-head (one wave per
 // query head), so each K/V tile is read from HBM once and reused G times
 // from LDS.  The split count depends only on the cache capacity, so a
@@ -93,8 +95,8 @@ __global__ __launch_bounds__(256) void rope_append_kernel(
 template <int D, int G>
 __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-    const int* __restrict__ lens, float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv,
-    int Smax, int splits, int chunk, float qscale) {
+    const int* __restrict__ lens, float* part_o, float* part_ml, unsigned* tickets,
+    bf16_t* __restrict__ out, int Hkv, int Smax, int splits, int chunk, float qscale) {
   constexpr int kPad = D + 8;
   constexpr int kPer = D / 64;  // output elements per lane
   __shared__ __attribute__((aligned(16))) float qs[G][D];
@@ -163,37 +165,66 @@ __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
       for (int t = 0; t < kPer; ++t) acc[t] += pj * bf2f(vs[j][lane + 64 * t]);
     }
   }
-  const int64_t row = (static_cast<int64_t>(b) * Hq + h) * splits + split;
+  const int64_t bh = static_cast<int64_t>(b) * Hq + h;
+  if (splits == 1) {
+    const float inv = l > 0.0f ? 1.0f / l : 0.0f;
 #pragma unroll
-  for (int t = 0; t < kPer; ++t) part_o[row * D + lane + 64 * t] = acc[t];
-  if (lane == 0) {
-    part_ml[row * 2] = m;
-    part_ml[row * 2 + 1] = l;
+    for (int t = 0; t < kPer; ++t) out[bh * D + lane + 64 * t] = f2bf(acc[t] * inv);
+    return;
   }
-}
-
-// Merge the per-split softmax states of one (b, h): one wave, lane d.
-template <int D>
-__global__ __launch_bounds__(64) void decode_combine_kernel(const float* __restrict__ part_o,
-                                                            const float* __restrict__ part_ml,
-                                                            bf16_t* __restrict__ out, int splits) {
-  constexpr int kPer = D / 64;
-  const int64_t bh = blockIdx.x;
-  const int lane = threadIdx.x;
-  float M = -INFINITY;
-  for (int s = 0; s < splits; ++s) M = fmaxf(M, part_ml[(bh * splits + s) * 2]);
-  float L = 0.0f, o[kPer];
+  // Publish this split's state with write-through (sc1) stores: relaxed
+  // agent-scope atomic stores, so another XCD's last arriver reads them
+  // from memory without any L2 writeback fence (cdna_hip_programming.md
+  // Guideline 16, R1).  A __threadfence() here instead cost 10x the kernel.
+  const int64_t row = bh * splits + split;
+#pragma unroll
+  for (int t = 0; t < kPer; ++t)
+    __hip_atomic_store(part_o + row * D + lane + 64 * t, acc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    __hip_atomic_store(part_ml + row * 2, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part_ml + row * 2 + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  __shared__ unsigned last;
+  if (threadIdx.x == 0) {
+    unsigned* tk = tickets + static_cast<int64_t>(b) * Hkv + kvh;
+    const unsigned n = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = n == static_cast<unsigned>(splits - 1);
+    // The ticket returns to 0 for the next call: every other split of this
+    // (b, kv head) has already added (stream order separates the calls).
+    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  // Last arriver: every split's state of each of the G heads (wave = head),
+  // all loads issued together as sc1 loads (relaxed agent-scope atomic
+  // loads: they bypass this CU's L1, so no acquire fence is needed — every
+  // load of the handed-off bytes is one, Guideline 16); lane sp holds split
+  // sp's (m, l).  Measured: 9.2 us for attention + merge, against 5.6 + 6.6
+  // for the two launches and 9.8 with an acquire fence and plain loads.
+  auto ld_sc1 = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const float ms = lane < splits ? ld_sc1(part_ml + (bh * splits + lane) * 2) : -INFINITY;
+  const float ls = lane < splits ? ld_sc1(part_ml + (bh * splits + lane) * 2 + 1) : 0.0f;
+  const float M = wave_max(ms);
+  const float w = ms == -INFINITY ? 0.0f : exp2f(ms - M);  // empty split (beyond the sequence): 0
+  const float L = wave_sum(w * ls);
+  float o[kPer];
 #pragma unroll
   for (int t = 0; t < kPer; ++t) o[t] = 0.0f;
-  if (M > -INFINITY) {
-    for (int s = 0; s < splits; ++s) {
-      const float ms = part_ml[(bh * splits + s) * 2];
-      if (ms == -INFINITY) continue;  // empty split (beyond the sequence)
-      const float w = exp2f(ms - M);
-      L += w * part_ml[(bh * splits + s) * 2 + 1];
+  for (int sp0 = 0; sp0 < splits; sp0 += 16) {
+    float ws[16], po[16][kPer];
 #pragma unroll
-      for (int t = 0; t < kPer; ++t) o[t] += w * part_o[(bh * splits + s) * D + lane + 64 * t];
+    for (int i = 0; i < 16; ++i) {
+      const int sp = min(sp0 + i, splits - 1);
+      ws[i] = sp0 + i < splits ? __shfl(w, sp, 64) : 0.0f;
+#pragma unroll
+      for (int t = 0; t < kPer; ++t) po[i][t] = ld_sc1(part_o + (bh * splits + sp) * D + lane + 64 * t);
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int t = 0; t < kPer; ++t) o[t] += ws[i] * po[i][t];
   }
   const float inv = L > 0.0f ? 1.0f / L : 0.0f;
 #pragma unroll
@@ -202,13 +233,11 @@ __global__ __launch_bounds__(64) void decode_combine_kernel(const float* __restr
 
 template <int D, int G>
 int launch_attn(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* lens, float* po,
-                float* pml, bf16_t* out, int B, int Hkv, int Smax, int splits, float scale,
-                hipStream_t st) {
+                float* pml, unsigned* tickets, bf16_t* out, int B, int Hkv, int Smax, int splits,
+                float scale, hipStream_t st) {
   const int chunk = ((Smax + splits - 1) / splits + 63) / 64 * 64;
   hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(splits, Hkv, B), dim3(64 * G), 0, st, q, kc,
-                     vc, lens, po, pml, Hkv, Smax, splits, chunk, scale * kLog2e);
-  hipLaunchKernelGGL((decode_combine_kernel<D>), dim3(B * Hkv * G), dim3(64), 0, st, po, pml, out,
-                     splits);
+                     vc, lens, po, pml, tickets, out, Hkv, Smax, splits, chunk, scale * kLog2e);
   return KGWE_CHECK_LAUNCH();
 }
 
@@ -226,9 +255,10 @@ KGWE_API int kgwe_decode_rope_append(const void* qkv, const int* pos, const floa
   return KGWE_CHECK_LAUNCH();
 }
 
-// Workspace floats: B * Hq * splits * (D + 2).
+// Workspace 4-byte words: B * Hq * splits * (D + 2) partials, then B * Hq
+// tickets (B * Hkv used).  Must be zeroed once when allocated.
 KGWE_API int64_t kgwe_decode_attn_workspace(int B, int Hq, int D, int splits) {
-  return static_cast<int64_t>(B) * Hq * splits * (D + 2);
+  return static_cast<int64_t>(B) * Hq * splits * (D + 2) + static_cast<int64_t>(B) * Hq;
 }
 
 // Split count for a cache of Smax keys: enough workgroups to cover the 256
@@ -236,7 +266,7 @@ KGWE_API int64_t kgwe_decode_attn_workspace(int B, int Hq, int D, int splits) {
 KGWE_API int kgwe_decode_attn_splits(int B, int Hkv, int Smax) {
   const int want = (512 + B * Hkv - 1) / (B * Hkv);
   const int most = (Smax + 63) / 64;
-  return std::max(1, std::min(want, most));
+  return std::max(1, std::min({want, most, 64}));  // the merge holds one split per lane
 }
 
 KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vcache, const int* lens,
@@ -246,12 +276,15 @@ KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vca
   const int G = Hq / Hkv;
   float* po = workspace;
   float* pml = workspace + static_cast<int64_t>(B) * Hq * splits * D;
+  // B * Hkv tickets after the partials; zero when the workspace is created,
+  // and returned to zero by every call's last arrivers.
+  auto tickets = reinterpret_cast<unsigned*>(pml + static_cast<int64_t>(B) * Hq * splits * 2);
   auto qp = static_cast<const bf16_t*>(q);
   auto kp = static_cast<const bf16_t*>(kcache);
   auto vp = static_cast<const bf16_t*>(vcache);
   auto op = static_cast<bf16_t*>(out);
 #define KGWE_DECODE_CASE(DD, GG) \
-  if (D == DD && G == GG) return launch_attn<DD, GG>(qp, kp, vp, lens, po, pml, op, B, Hkv, Smax, splits, scale, st);
+  if (D == DD && G == GG) return launch_attn<DD, GG>(qp, kp, vp, lens, po, pml, tickets, op, B, Hkv, Smax, splits, scale, st);
   KGWE_DECODE_CASE(64, 1)
   KGWE_DECODE_CASE(64, 2)
   KGWE_DECODE_CASE(64, 4)
