@@ -98,9 +98,10 @@ class Generator:
     # ------------------------------------------------------------ decode
     @torch.no_grad()
     def _step_fused(self) -> None:
-        """One decode step in 5 projection kernels per layer + RoPE/append +
-        attention: [RMSNorm(+res) -> wqkv], wo, [RMSNorm(+res) -> w13 -> SwiGLU],
-        w2, and [RMSNorm(+res) -> LM head -> argmax] at the end."""
+        """One decode step in 5 kernels per layer: [RMSNorm(+res) -> wqkv],
+        [RoPE + KV append + split-K attention + merge], wo,
+        [RMSNorm(+res) -> w13 -> SwiGLU], w2; and [RMSNorm(+res) -> LM head ->
+        argmax] at the end."""
         c, m = self.cfg, self.m
         hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
         B, eps = self.B, c.norm_eps
@@ -115,8 +116,7 @@ class Generator:
             else:
                 qkv = dec.gemv(x, at.wqkv, dec.GEMV_NORM, res=res, g=layer.attention_norm, eps=eps, h_out=hA)
                 h = hA
-            q = dec.rope_append(qkv, self.pos, self.cos, self.sin, self.kv[0, i], self.kv[1, i], hq, hkv, d)
-            o = self.attn(q, self.kv[0, i], self.kv[1, i], self.lens)
+            o = self.attn.rope_attend(qkv, self.cos, self.sin, self.kv[0, i], self.kv[1, i], self.lens)
             a = dec.gemv(o.view(B, -1), at.wo)
             f = dec.gemv(a, ff.w13, dec.GEMV_NORM_SWIGLU, res=h, g=layer.ffn_norm, eps=eps, h_out=hB)
             x = dec.gemv(f, ff.w2) if self.w2_fused else K.linear(f, ff.w2)

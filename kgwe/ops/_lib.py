@@ -50,6 +50,8 @@ _SIGS = {
                                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "kgwe_decode_attn": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                  c_int, c_int, c_int, c_int, c_int, c_float, c_void_p]),
+    "kgwe_decode_attn_rope": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p]),
     "kgwe_decode_attn_workspace": (c_int64, [c_int, c_int, c_int, c_int]),
     "kgwe_decode_attn_splits": (c_int, [c_int, c_int, c_int]),
     "kgwe_decode_gemv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,

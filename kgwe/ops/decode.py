@@ -114,6 +114,30 @@ class DecodeAttention:
         return out
 
 
+    def rope_attend(self, qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, kc: torch.Tensor,
+                    vc: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+        """``rope_append`` + ``__call__`` in one launch: qkv [B, (hq+2hkv)d] of
+        the new token at position lens - 1; RoPE'd k and v are appended to the
+        caches there.  Returns [B, hq, d]."""
+        if not self.hip:
+            q = rope_append_reference(qkv, lens - 1, cos, sin, kc, vc, self.hq, self.hkv, self.d)
+            return decode_attention_reference(q, kc, vc, lens)
+        B, hq, hkv, d = self.B, self.hq, self.hkv, self.d
+        _require(qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and qkv.shape == (B, (hq + 2 * hkv) * d),
+                 "decode_attention: qkv must be contiguous bf16 [B, (hq+2hkv)*d]")
+        _require(kc.shape == vc.shape == (B, hkv, self.smax, d) and kc.is_contiguous() and vc.is_contiguous(),
+                 "decode_attention: cache shape")
+        _require(lens.dtype == torch.int32 and lens.shape == (B,), "decode_attention: lens int32 [B]")
+        _require(cos.dtype == sin.dtype == torch.float32 and cos.shape == sin.shape
+                 and cos.shape[0] >= self.smax and cos.shape[1] == d // 2 and cos.is_contiguous()
+                 and sin.is_contiguous(), "decode_attention: cos/sin fp32 [>=Smax, d/2]")
+        out = torch.empty(B, hq, d, device=qkv.device, dtype=qkv.dtype)
+        check(lib().kgwe_decode_attn_rope(ptr(qkv), ptr(cos), ptr(sin), ptr(kc), ptr(vc), ptr(lens),
+                                          ptr(self.work), ptr(out), B, hq, hkv, d, self.smax, self.splits,
+                                          1.0 / math.sqrt(d), stream(qkv)), "decode_attn_rope")
+        return out
+
+
 # ------------------------------------------------------------------ projections
 GEMV_PLAIN, GEMV_NORM, GEMV_SWIGLU, GEMV_NORM_SWIGLU, GEMV_NORM_ARGMAX = 0, 1, 2, 3, 5
 GEMV_M = (1, 2, 4, 8)

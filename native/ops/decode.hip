@@ -92,11 +92,19 @@ __global__ __launch_bounds__(256) void rope_append_kernel(
 // from LDS as a broadcast); online softmax in the exp2 domain (q pre-scaled
 // by softmax_scale * log2 e); then lane d accumulates sum_j p_j V[j][d].
 // ---------------------------------------------------------------------------
-template <int D, int G>
+//
+// ROPE: q is the fused projection output qkv [B, (Hq + 2 Hkv) * D] of the new
+// token at position p = lens[b] - 1, and this kernel also does the work of
+// rope_append_kernel: RoPE of the G query heads in the prologue, and in the
+// one split whose key range holds p, RoPE of the new key + the cache append
+// of k and v (the staging thread of each chunk of row p computes it, stores
+// it to the cache and to LDS), with the same roundings.  One launch less per
+// layer.
+template <int D, int G, bool ROPE>
 __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-    const int* __restrict__ lens, float* part_o, float* part_ml, unsigned* tickets,
-    bf16_t* __restrict__ out, int Hkv, int Smax, int splits, int chunk, float qscale) {
+    const bf16_t* __restrict__ q, bf16_t* kc, bf16_t* vc, const float* __restrict__ cosT,
+    const float* __restrict__ sinT, const int* __restrict__ lens, float* part_o, float* part_ml,
+    unsigned* tickets, bf16_t* __restrict__ out, int Hkv, int Smax, int splits, int chunk, float qscale) {
   constexpr int kPad = D + 8;
   constexpr int kPer = D / 64;  // output elements per lane
   __shared__ __attribute__((aligned(16))) float qs[G][D];
@@ -110,12 +118,26 @@ __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
   const int len = min(lens[b], Smax);
   const int start = split * chunk;
   const int end = min(len, start + chunk);
-  const bf16_t* qrow = q + (static_cast<int64_t>(b) * Hq + h) * D;
+  constexpr int half = D / 2;
+  const int Ht = Hq + 2 * Hkv;
+  const int p = min(max(lens[b] - 1, 0), Smax - 1);  // ROPE: the new token's position
+  if (ROPE) {
+    const bf16_t* qrow = q + (static_cast<int64_t>(b) * Ht + h) * D;
 #pragma unroll
-  for (int t = 0; t < kPer; ++t) qs[wave][lane + 64 * t] = bf2f(qrow[lane + 64 * t]) * qscale;
+    for (int t = 0; t < kPer; ++t) {
+      const int i = lane + 64 * t, j = i < half ? i : i - half;
+      const float x = bf2f(qrow[i]), y = bf2f(qrow[i < half ? i + half : i - half]);
+      const float cs = cosT[static_cast<int64_t>(p) * half + j], sn = sinT[static_cast<int64_t>(p) * half + j];
+      qs[wave][i] = bf2f(f2bf(i < half ? x * cs - y * sn : x * cs + y * sn)) * qscale;  // as rope_append_kernel
+    }
+  } else {
+    const bf16_t* qrow = q + (static_cast<int64_t>(b) * Hq + h) * D;
+#pragma unroll
+    for (int t = 0; t < kPer; ++t) qs[wave][lane + 64 * t] = bf2f(qrow[lane + 64 * t]) * qscale;
+  }
   const int64_t slab = (static_cast<int64_t>(b) * Hkv + kvh) * Smax * D;
-  const bf16_t* kbase = kc + slab;
-  const bf16_t* vbase = vc + slab;
+  bf16_t* kbase = kc + slab;
+  bf16_t* vbase = vc + slab;
   float m = -INFINITY, l = 0.0f;
   float acc[kPer];
 #pragma unroll
@@ -127,7 +149,24 @@ __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
       const int r = idx / (D / 8), c = (idx % (D / 8)) * 8;
       const int key = t0 + r;
       bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (key < end) {
+      if (ROPE && key == p && key < end) {
+        // the new token: RoPE of k (a chunk lies in one half), v as is; append both
+        const bf16_t* kin = q + (static_cast<int64_t>(b) * Ht + Hq + kvh) * D;
+        const bf16_t* vin = q + (static_cast<int64_t>(b) * Ht + Hq + Hkv + kvh) * D;
+        const int cj = c < half ? c : c - half;
+        const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(kin + cj);
+        const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(kin + cj + half);
+        const float* cp = cosT + static_cast<int64_t>(p) * half + cj;
+        const float* sp = sinT + static_cast<int64_t>(p) * half + cj;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = bf2f(x0[j]), bb = bf2f(x1[j]);
+          kv[j] = f2bf(c < half ? a * cp[j] - bb * sp[j] : bb * cp[j] + a * sp[j]);
+        }
+        vv = *reinterpret_cast<const bf16x8*>(vin + c);
+        *reinterpret_cast<bf16x8*>(kbase + static_cast<int64_t>(key) * D + c) = kv;
+        *reinterpret_cast<bf16x8*>(vbase + static_cast<int64_t>(key) * D + c) = vv;
+      } else if (key < end) {
         kv = *reinterpret_cast<const bf16x8*>(kbase + static_cast<int64_t>(key) * D + c);
         vv = *reinterpret_cast<const bf16x8*>(vbase + static_cast<int64_t>(key) * D + c);
       }
@@ -232,12 +271,16 @@ __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
 }
 
 template <int D, int G>
-int launch_attn(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int* lens, float* po,
-                float* pml, unsigned* tickets, bf16_t* out, int B, int Hkv, int Smax, int splits,
-                float scale, hipStream_t st) {
+int launch_attn(const bf16_t* q, bf16_t* kc, bf16_t* vc, const float* cosT, const float* sinT,
+                const int* lens, float* po, float* pml, unsigned* tickets, bf16_t* out, int B, int Hkv,
+                int Smax, int splits, float scale, hipStream_t st) {
   const int chunk = ((Smax + splits - 1) / splits + 63) / 64 * 64;
-  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(splits, Hkv, B), dim3(64 * G), 0, st, q, kc,
-                     vc, lens, po, pml, tickets, out, Hkv, Smax, splits, chunk, scale * kLog2e);
+  if (cosT != nullptr)
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, true>), dim3(splits, Hkv, B), dim3(64 * G), 0, st, q, kc,
+                       vc, cosT, sinT, lens, po, pml, tickets, out, Hkv, Smax, splits, chunk, scale * kLog2e);
+  else
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, false>), dim3(splits, Hkv, B), dim3(64 * G), 0, st, q, kc,
+                       vc, cosT, sinT, lens, po, pml, tickets, out, Hkv, Smax, splits, chunk, scale * kLog2e);
   return KGWE_CHECK_LAUNCH();
 }
 
@@ -269,9 +312,10 @@ KGWE_API int kgwe_decode_attn_splits(int B, int Hkv, int Smax) {
   return std::max(1, std::min({want, most, 64}));  // the merge holds one split per lane
 }
 
-KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vcache, const int* lens,
-                              float* workspace, void* out, int B, int Hq, int Hkv, int D, int Smax,
-                              int splits, float scale, hipStream_t st) {
+namespace {
+int decode_attn_impl(const void* q, void* kcache, void* vcache, const float* cos_t, const float* sin_t,
+                     const int* lens, float* workspace, void* out, int B, int Hq, int Hkv, int D, int Smax,
+                     int splits, float scale, hipStream_t st) {
   if (B <= 0 || Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || Smax <= 0) return -1;
   const int G = Hq / Hkv;
   float* po = workspace;
@@ -280,11 +324,13 @@ KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vca
   // and returned to zero by every call's last arrivers.
   auto tickets = reinterpret_cast<unsigned*>(pml + static_cast<int64_t>(B) * Hq * splits * 2);
   auto qp = static_cast<const bf16_t*>(q);
-  auto kp = static_cast<const bf16_t*>(kcache);
-  auto vp = static_cast<const bf16_t*>(vcache);
+  auto kp = static_cast<bf16_t*>(kcache);
+  auto vp = static_cast<bf16_t*>(vcache);
   auto op = static_cast<bf16_t*>(out);
-#define KGWE_DECODE_CASE(DD, GG) \
-  if (D == DD && G == GG) return launch_attn<DD, GG>(qp, kp, vp, lens, po, pml, tickets, op, B, Hkv, Smax, splits, scale, st);
+#define KGWE_DECODE_CASE(DD, GG)                                                                        \
+  if (D == DD && G == GG)                                                                               \
+    return launch_attn<DD, GG>(qp, kp, vp, cos_t, sin_t, lens, po, pml, tickets, op, B, Hkv, Smax, splits, \
+                               scale, st);
   KGWE_DECODE_CASE(64, 1)
   KGWE_DECODE_CASE(64, 2)
   KGWE_DECODE_CASE(64, 4)
@@ -295,4 +341,22 @@ KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vca
   KGWE_DECODE_CASE(128, 8)
 #undef KGWE_DECODE_CASE
   return -2;  // unsupported (head_dim, group) combination
+}
+}  // namespace
+
+KGWE_API int kgwe_decode_attn(const void* q, const void* kcache, const void* vcache, const int* lens,
+                              float* workspace, void* out, int B, int Hq, int Hkv, int D, int Smax,
+                              int splits, float scale, hipStream_t st) {
+  return decode_attn_impl(q, const_cast<void*>(kcache), const_cast<void*>(vcache), nullptr, nullptr, lens,
+                          workspace, out, B, Hq, Hkv, D, Smax, splits, scale, st);
+}
+
+// RoPE + cache append + attention in one launch: qkv [B, (Hq + 2 Hkv) * D] of
+// the new token at position lens[b] - 1; cos/sin fp32 [>= Smax, D / 2].
+KGWE_API int kgwe_decode_attn_rope(const void* qkv, const float* cos_t, const float* sin_t, void* kcache,
+                                   void* vcache, const int* lens, float* workspace, void* out, int B, int Hq,
+                                   int Hkv, int D, int Smax, int splits, float scale, hipStream_t st) {
+  if (cos_t == nullptr || sin_t == nullptr) return -1;
+  return decode_attn_impl(qkv, kcache, vcache, cos_t, sin_t, lens, workspace, out, B, Hq, Hkv, D, Smax,
+                          splits, scale, st);
 }

@@ -57,6 +57,39 @@ def test_rope_append_matches_reference():
     assert torch.equal(vc.cpu(), vr)
 
 
+@pytest.mark.parametrize("B,hq,hkv,d,smax,lens", [
+    (3, 32, 8, 64, 300, [1, 77, 300]),     # new token in the first / a middle / the last split
+    (2, 16, 4, 128, 1030, [1030, 514]),
+    (4, 8, 8, 64, 129, [128, 129, 2, 64]),
+])
+def test_fused_rope_attention_matches_separate_kernels(B, hq, hkv, d, smax, lens):
+    """rope_attend (RoPE + KV append + attention + in-kernel split merge, one
+    launch) against rope_append + the attention launch: same appended cache
+    rows, same output, and the split tickets reset between calls."""
+    from kgwe.ops import decode as dec
+    from kgwe.ops import reference as ref
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    qkv = torch.randn(B, (hq + 2 * hkv) * d, device="cuda", generator=g).to(torch.bfloat16)
+    kc = torch.randn(B, hkv, smax, d, device="cuda", generator=g).to(torch.bfloat16)
+    vc = torch.randn(B, hkv, smax, d, device="cuda", generator=g).to(torch.bfloat16)
+    cos, sin = ref.rope_tables(smax, d, 500000.0, "cuda")
+    cos, sin = cos.float().contiguous(), sin.float().contiguous()
+    ln = torch.tensor(lens, device="cuda", dtype=torch.int32)
+    att = dec.DecodeAttention(B, hq, hkv, d, smax, "cuda")
+    k1, v1 = kc.clone(), vc.clone()
+    q = dec.rope_append(qkv, ln - 1, cos, sin, k1, v1, hq, hkv, d)
+    want = att(q, k1, v1, ln).float()
+    for _ in range(2):  # twice: the tickets must be back at zero after a call
+        k2, v2 = kc.clone(), vc.clone()
+        got = att.rope_attend(qkv, cos, sin, k2, v2, ln).float()
+        assert torch.equal(k2, k1) and torch.equal(v2, v1)
+        err = (got - want).abs().max().item()
+        assert err < 1e-2, err
+    ref_o = dec.decode_attention_reference(q, k1, v1, ln).float()
+    assert (got - ref_o).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("M,N,K,mode", [
     (1, 384, 2048, 0), (4, 3072, 2048, 1), (8, 520, 2048, 1), (4, 2048, 8192, 0),
     (2, 1024, 2048, 3), (4, 4096, 2048, 3), (4, 20000, 2048, 1), (4, 96, 64, 2),
