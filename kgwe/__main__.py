@@ -14,6 +14,7 @@ COMMANDS = {
     "bench-scale": "kgwe.bench.scale",  # scheduling core on a 10k-GPU fleet
     "bench-cluster": "kgwe.bench.cluster",  # stock kube vs kgwe on one trace (simulated)
     "bench-scaling": "kgwe.bench.scaling",  # bench.py at 1/2/4/8 GPUs -> scaling curve
+    "bench-infer": "kgwe.bench.infer",  # bf16 decode server / co-located servers on one GPU
     "busbw": "kgwe.parallel.busbw",            # RCCL all-reduce bus bandwidth sweep
     "crds": "kgwe.api.crds",                   # render CRD YAML
     "launch": "kgwe.launch",                   # container entrypoint (placement env)
