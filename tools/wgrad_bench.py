@@ -51,6 +51,11 @@ def main():
             "gemm_tt": lambda: torch.mm(dy.t(), xT.t()),
             "gemm_nn": lambda: torch.mm(dyT, x),
             "gemm_nt": lambda: torch.mm(dyT, xT.t()),
+            # dW^T = X^T dY (the other output orientation; same operands)
+            "rawT": lambda: torch.mm(x.t(), dy),
+            "T_tt": lambda: torch.mm(x.t(), dyT.t()),
+            "T_nn": lambda: torch.mm(xT, dy),
+            "T_nt": lambda: torch.mm(xT, dyT.t()),
             "tr_dy": lambda: F.transpose(dy),
             "tr_x": lambda: F.transpose(x),
         }
