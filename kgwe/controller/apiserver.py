@@ -176,8 +176,13 @@ class _Handler(BaseHTTPRequestHandler):
                 return self._send(404, {"reason": "NotFound"})
             if pod.get("spec", {}).get("nodeName"):
                 return self._send(409, {"reason": "Conflict", "message": "pod already bound"})
-            st.patch("pods", d["ns"], d["name"], {"spec": {"nodeName": node},
-                                                  "status": {"phase": "Running"}})
+            # kube-apiserver's binding REST copies the Binding's annotations
+            # onto the pod together with spec.nodeName (one write).
+            patch = {"spec": {"nodeName": node}, "status": {"phase": "Running"}}
+            ann = (body.get("metadata") or {}).get("annotations")
+            if ann:
+                patch["metadata"] = {"annotations": ann}
+            st.patch("pods", d["ns"], d["name"], patch)
             return self._send(201, {"kind": "Status", "status": "Success"})
         o = st.create(d["coll"], d["ns"], body)
         if o is None:

@@ -135,9 +135,15 @@ class KubeClient:
         return self.request("PATCH", f"/api/v1/namespaces/{namespace}/pods/{name}", patch,
                             content_type="application/merge-patch+json")
 
-    def bind_pod(self, namespace: str, name: str, node: str, uid: str = "") -> dict:
-        body = {"apiVersion": "v1", "kind": "Binding",
-                "metadata": {"name": name, "namespace": namespace, "uid": uid},
+    def bind_pod(self, namespace: str, name: str, node: str, uid: str = "",
+                 annotations: dict | None = None) -> dict:
+        """pods/binding.  The apiserver copies the Binding's annotations onto
+        the pod in the same write as spec.nodeName (BindingREST), so placement
+        annotations need no separate PATCH round trip."""
+        meta = {"name": name, "namespace": namespace, "uid": uid}
+        if annotations:
+            meta["annotations"] = annotations
+        body = {"apiVersion": "v1", "kind": "Binding", "metadata": meta,
                 "target": {"apiVersion": "v1", "kind": "Node", "name": node}}
         return self.request("POST", f"/api/v1/namespaces/{namespace}/pods/{name}/binding", body)
 
