@@ -439,7 +439,10 @@ def test_controller_consolidates_partitions_by_eviction():
         assert m["slice_utilization"] == pytest.approx(6 / 8)
         moved = [n for n in (f"inf-{i}" for i in range(12)) if _status(kube, "ml", n).get("migrations")]
         assert moved and rec.migrations == len(moved)
-        assert all(_status(kube, "ml", n)["phase"] in ("Scheduled", "Running") for n in moved)
+        # the ledger holds the re-placed slice before the reconciler writes the
+        # CR status, so wait for the status instead of sampling it once
+        wait_for(lambda: all(_status(kube, "ml", n).get("phase") in ("Scheduled", "Running")
+                             for n in moved), timeout=20)
         assert rec.errors == 0
     finally:
         stop()
