@@ -71,6 +71,8 @@ def parse(argv=None):
     ap.add_argument("--no-cluster", action="store_true",
                     help="skip the stock-kube vs kgwe cluster simulation row")
     ap.add_argument("--no-busbw", action="store_true", help="skip the RCCL all-reduce busBW probe")
+    ap.add_argument("--no-xgmi-probe", action="store_true",
+                    help="skip the per-link xGMI bandwidth probe the launcher runs at N > 1")
     ap.add_argument("--sdpa", action="store_true", help="force PyTorch SDPA attention")
     ap.add_argument("--parallel", default="zero", choices=["zero", "fsdp"],
                     help="headline row. zero: replicated bf16 weights + sharded fp32 "
@@ -93,12 +95,35 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def xgmi_probe(n: int, env: dict) -> dict | None:
+    """Per-link xGMI bandwidth of the GPUs the job runs on (N1: the HIP
+    LDS-staged peer-pull probe), in a child process that finishes before any
+    rank starts, so it never shares the GPUs with training."""
+    import subprocess
+
+    try:
+        r = subprocess.run([sys.executable, "-m", "kgwe.agent.probes", "--xgmi", str(n)], cwd=HERE,
+                           env=env, capture_output=True, text=True, timeout=180)
+        js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not js:
+            raise RuntimeError(f"rc={r.returncode}: {r.stderr[-300:]}")
+        return json.loads(js[-1]).get("xgmi")
+    except Exception as e:  # noqa: BLE001 - optional row, reported, never faked
+        print(f"[bench] xGMI probe failed: {e}", file=sys.stderr, flush=True)
+        return {"error": str(e)[:300]}
+
+
 def launch(args, argv: list[str]) -> int:
     """Parent: spawn N ranks under torch.distributed.run, never touch the GPU."""
     import subprocess
     import threading
 
     n = max(1, args.gpus)
+    probe = None
+    if n > 1 and not args.no_xgmi_probe:
+        env0 = dict(os.environ)
+        env0.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        probe = xgmi_probe(n, env0)
     port = _free_port()
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
@@ -132,6 +157,8 @@ def launch(args, argv: list[str]) -> int:
         print(f"[bench] rank 0 reported n_gpus={out.get('n_gpus')} for --gpus {n}", file=sys.stderr)
         return 1
     out["launcher"] = f"bench.py -> torch.distributed.run --nproc-per-node {n} (child process)"
+    if probe is not None:
+        out["xgmi_probe"] = probe
     print(json.dumps(out), flush=True)
     return 0
 

@@ -73,3 +73,58 @@ def probe_p2p_all(ndev: int, nbytes: int = 128 << 20, iters: int = 5) -> list[li
     if rc < 0:
         raise RuntimeError(f"kgwe_probe_p2p_all failed rc={rc}")
     return [[mat[d * ndev + s] for s in range(ndev)] for d in range(ndev)]
+
+
+def _stats(xs: list[float]) -> dict:
+    xs = sorted(x for x in xs if x > 0)
+    if not xs:
+        return {"links": 0}
+    return {"links": len(xs), "min_gbps": round(xs[0], 1), "median_gbps": round(xs[len(xs) // 2], 1),
+            "max_gbps": round(xs[-1], 1)}
+
+
+def xgmi_report(ndev: int, pair_bytes: int = 256 << 20, all_bytes: int = 128 << 20) -> dict:
+    """One link at a time (GPU 0 pulling from each peer, and each peer pulling
+    from GPU 0), then every ordered pair at once: the per-link numbers the
+    agent attaches to the topology, measured on the node the job runs on."""
+    ndev = min(ndev, device_count())
+    if ndev < 2:
+        return {"devices": ndev, "error": "needs >= 2 visible GPUs"}
+    single = {}
+    for p in range(1, ndev):
+        for src, dst in ((p, 0), (0, p)):
+            try:
+                g = probe_p2p(src, dst, pair_bytes, 10)
+            except RuntimeError:  # peer access refused: reported as an unmeasured link
+                g = None
+            single[f"{src}->{dst}"] = round(g, 1) if g is not None else None
+    mat = probe_p2p_all(ndev, all_bytes, 5)
+    per_gpu_in = [round(sum(row), 1) for row in mat]
+    return {"devices": ndev, "kernel": "lds_pull_kernel (global_load_lds, peer HBM -> LDS -> local HBM)",
+            "single_link_gbps": single,
+            "single_link": _stats([v for v in single.values() if v is not None]),
+            "all_links": _stats([mat[d][s] for d in range(ndev) for s in range(ndev) if s != d]),
+            "all_links_ingress_per_gpu_gbps": per_gpu_in,
+            "matrix_gbps": [[round(x, 1) for x in row] for row in mat]}
+
+
+def main(argv=None) -> int:
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser(description="HIP HBM / xGMI bandwidth probes")
+    ap.add_argument("--xgmi", type=int, default=0, metavar="N",
+                    help="probe the xGMI links among the first N GPUs")
+    ap.add_argument("--hbm", type=int, default=-1, metavar="DEV", help="HBM self-probe of one GPU")
+    a = ap.parse_args(argv)
+    out = {}
+    if a.hbm >= 0:
+        out["hbm"] = probe_hbm(a.hbm, 1 << 30, 10).__dict__
+    if a.xgmi > 0:
+        out["xgmi"] = xgmi_report(a.xgmi)
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -43,7 +43,7 @@ _SIGS = {
     "kgwe_cross_entropy_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int64, c_int64, c_int64, c_void_p]),
     "kgwe_adamw_step": (c_int, [c_void_p, c_int, c_float, c_float, c_float, c_float,
-                                c_float, c_int, c_float, c_void_p]),
+                                c_float, c_int, c_float, c_int, c_void_p]),
     "kgwe_transpose_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
     "kgwe_adamw_chunk_elems": (c_int, []),
     "kgwe_decode_rope_append": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -67,14 +67,16 @@ class AdamPlan:
                        int(g.dtype == torch.bfloat16), 0)
         return tens
 
-    def launch(self, entries, lr, b1, b2, eps, wd, step, grad_scale=1.0):
+    def launch(self, entries, lr, b1, b2, eps, wd, step, grad_scale=1.0, max_grid=0):
+        """max_grid > 0 caps the workgroups per launch (a background update
+        beside other kernels; see kgwe_adamw_step)."""
         if not entries:
             return
         p0 = entries[0][0]
         if p0.is_cuda:
             tens = self.records(entries)
             check(lib().kgwe_adamw_step(tens.ctypes.data, len(entries), lr, b1, b2, eps, wd,
-                                        step, grad_scale, stream(p0)), "adamw_step")
+                                        step, grad_scale, int(max_grid), stream(p0)), "adamw_step")
             return
         for p, g, m, v, sh in entries:
             gg = g.float() * grad_scale if grad_scale != 1.0 else g.float()

@@ -40,6 +40,7 @@ training-side implementation the platform places.
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -80,7 +81,7 @@ class ShardedDataParallel:
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, bucket_elems: int = 100 * 2**20,
                  reduce_dtype: torch.dtype = torch.float32, group=None, overlap_step: bool = True,
-                 transposed_weights: bool = True):
+                 transposed_weights: bool = True, background_grid: int | None = None):
         self.model = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.group = group
@@ -88,6 +89,16 @@ class ShardedDataParallel:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.reduce_dtype = reduce_dtype
         self.overlap = overlap_step
+        # Workgroup cap of the AdamW launches that run BESIDE backward (every
+        # bucket but the last to complete).  A full-grid HBM-bound update
+        # co-resides on every CU and roughly doubles the GEMM next to it
+        # (tools/gemm_instep.py), but a capped grid only stretches the damage
+        # over more GEMMs: 699 ms/step uncapped, 701 / 723 / 777 / 882 at
+        # 1024 / 256 / 128 / 64 workgroups (profiles/r02_step/SUMMARY.md).
+        # Kept as a knob; 0 = no cap (default).
+        if background_grid is None:
+            background_grid = int(os.environ.get("KGWE_ADAMW_BG_GRID", "0"))
+        self.background_grid = max(0, background_grid)
         self._step = 0
         self._armed = False  # this iteration's step counter already advanced
         # events every writer of master / m / v / flat must wait for before the
@@ -208,17 +219,20 @@ class ShardedDataParallel:
         if self.world > 1:
             self._reduce_scatter(b)
         if self.overlap:
-            self._update(b)
+            # buckets complete in list order; the last one has no backward left to hide behind
+            self._update(b, background=b is not self.buckets[-1])
 
     def _reduce_scatter(self, b: _Bucket) -> None:
         b.rs_work = dist.reduce_scatter_tensor(b.gshard, b.gfull, op=dist.ReduceOp.SUM,
                                                group=self.group, async_op=True)
 
     @torch.no_grad()
-    def _update(self, b: _Bucket) -> None:
+    def _update(self, b: _Bucket, background: bool = False) -> None:
         """AdamW on this rank's part of bucket ``b`` (+ all-gather for world
-        > 1), on the side stream when there is one."""
+        > 1), on the side stream when there is one; ``background``: capped
+        grid (backward still running beside it)."""
         b1, b2 = self.betas
+        grid = self.background_grid if background else 0
         side = self._side
         if side is not None:
             side.wait_stream(torch.cuda.current_stream(self.device))
@@ -234,7 +248,7 @@ class ShardedDataParallel:
                 s0 = self.rank * b.shard
                 self._plan.launch([(b.master, b.gshard, b.m, b.v, b.flat[s0:s0 + b.shard])],
                                   self.lr, b1, b2, self.eps, self.wd, self._step,
-                                  grad_scale=1.0 / self.world)
+                                  grad_scale=1.0 / self.world, max_grid=grid)
                 b.ag_work = dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard],
                                                         group=self.group, async_op=True)
                 if b.tparams and side is not None:
@@ -256,7 +270,8 @@ class ShardedDataParallel:
                     entries.append((b.master[o:o + n], g.view(-1), b.m[o:o + n], b.v[o:o + n],
                                     b.flat[o:o + n]))
                     p.grad = None
-                self._plan.launch(entries, self.lr, b1, b2, self.eps, self.wd, self._step)
+                self._plan.launch(entries, self.lr, b1, b2, self.eps, self.wd, self._step,
+                                  max_grid=grid)
                 self._refresh_transposed(b)
                 if side is not None:
                     b.ready = torch.cuda.Event()
@@ -323,6 +338,7 @@ class ShardedDataParallel:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+
         for b in self.buckets:
             for p in b.params:
                 p.grad = None

@@ -135,8 +135,15 @@ KGWE_API int kgwe_adamw_tensor_bytes() { return sizeof(AdamTensor); }
 // `tensors`: HOST array of n AdamTensor records (device pointers inside).
 // `step` is the 1-based step count after increment (bias corrections are
 // computed here; no device sync).  Launches ceil(n / 16) kernels on `s`.
+// `max_grid` caps the workgroups of a launch (<= 0: 4096, enough to run at
+// the HBM limit).  A small cap makes the update a BACKGROUND kernel: issued
+// on a side stream beside the backward GEMMs, 4096 workgroups of a
+// memory-bound kernel co-reside on every CU and slow the GEMM next to them
+// ~2x (tools/gemm_instep.py); a few hundred grid-striding workgroups take
+// longer but leave most CUs to the GEMM.
 KGWE_API int kgwe_adamw_step(const void* tensors, int n, float lr, float b1, float b2, float eps,
-                             float wd, int step, float grad_scale, hipStream_t s) {
+                             float wd, int step, float grad_scale, int max_grid, hipStream_t s) {
+  const int cap = max_grid > 0 ? max_grid : 4096;
   if (n <= 0) return 0;
   AdamArgs a;
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
@@ -155,7 +162,7 @@ KGWE_API int kgwe_adamw_step(const void* tensors, int n, float lr, float b1, flo
       b.chunk_end[b.n] = acc;
       ++b.n;
     }
-    const int grid = acc < 4096 ? static_cast<int>(acc) : 4096;
+    const int grid = acc < cap ? static_cast<int>(acc) : cap;
     hipLaunchKernelGGL(adamw_kernel, dim3(grid), dim3(256), 0, s, b, a);
     const int rc = KGWE_CHECK_LAUNCH();
     if (rc) return rc;

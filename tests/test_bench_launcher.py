@@ -40,6 +40,8 @@ def test_bench_gpus2_spawns_two_gloo_ranks():
     assert out["fsdp_row"]["parallelism"] == "fsdp2"
     assert out["fsdp_row"]["tokens_per_s"] > 0
     assert out["tokens_per_s"] > 0 and out["ms_per_step"] > 0
+    # the launcher's per-link xGMI probe ran (a CPU host has no GPUs to probe)
+    assert "xgmi_probe" in out and out["xgmi_probe"].get("devices", 0) < 2
 
 
 def test_bench_failing_rank_fails_the_launcher():
