@@ -44,6 +44,21 @@ def test_bench_gpus2_spawns_two_gloo_ranks():
     assert "xgmi_probe" in out and out["xgmi_probe"].get("devices", 0) < 2
 
 
+def test_bench_gpus4_rehearses_the_multi_rank_path():
+    """Four gloo ranks through the same launcher (the driver's N=4 point): the
+    sharded-DP headline row and the FSDP2 row both run and every rank
+    reports (the busBW sweep is off: 1 GiB all-reduces on gloo)."""
+    r, lines = _run(4, ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1",
+                        "--fsdp-row", "on"], timeout=400)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(lines[-1])
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "zero2-dp4"
+    assert out["config"]["global_batch"] == 4
+    assert len(out["loss_per_rank"]) == 4 and len(set(out["loss_per_rank"])) == 4
+    assert out["fsdp_row"]["parallelism"] == "fsdp4" and "error" not in out["fsdp_row"]
+    assert out["config"]["grad_reduce_dtype"] == "fp32"
+
+
 def test_bench_failing_rank_fails_the_launcher():
     # An impossible model name makes every rank raise: the launcher must exit
     # non-zero and print no result line.
