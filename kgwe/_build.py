@@ -38,6 +38,12 @@ HIP_FLAGS = [
     "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
     "-munsafe-fp-atomics",
 ]
+# Per-source extras.  flash_attn.hip: no SLP vectorisation — hipcc otherwise
+# packs the softmax's adjacent f32 adds / multiplies into v_pk_*_f32, which
+# costs more than two plain VALU ops when issued beside MFMAs
+# (MI355X_MICROARCH.md); outputs are bit-identical, fwd / bwd +0.5-1 %
+# (tools/gpu_fa_variants.sh "noslp").
+HIP_FILE_FLAGS = {"flash_attn.hip": ["-fno-slp-vectorize"]}
 CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wextra",
              "-Wno-unused-parameter"]
 
@@ -87,7 +93,8 @@ def build_ops(force: bool = False, jobs: int = 8) -> Path:
     srcs = _sources("ops")
     inc = [ROOT / "native" / "ops"]
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, HIPCC, HIP_FLAGS, inc, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, HIPCC, HIP_FLAGS + HIP_FILE_FLAGS.get(s.name, []),
+                                              inc, force), srcs))
     return _link(objs, LIB / "libkgwe_ops.so", HIPCC,
                  [f"--offload-arch={ARCH}", "-lamdhip64"], force)
 

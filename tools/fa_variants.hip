@@ -61,11 +61,13 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(v, hv.data(), nkv * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(dout, hdo.data(), nq * 2, hipMemcpyHostToDevice));
   const float scale = 1.0f / std::sqrt(float(D));
+  // FA_CAUSAL=0 in the environment times the full (non-causal) problem
+  const int causal = std::getenv("FA_CAUSAL") ? std::atoi(std::getenv("FA_CAUSAL")) : 1;
   auto fwd = [&]() {
-    if (kgwe_flash_attn_fwd(q, k, v, o, lse, B, S, H, HKV, D, scale, 1, 0)) std::exit(2);
+    if (kgwe_flash_attn_fwd(q, k, v, o, lse, B, S, H, HKV, D, scale, causal, 0)) std::exit(2);
   };
   auto bwd = [&]() {
-    if (kgwe_flash_attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, work, nullptr, B, S, H, HKV, D, scale, 1, 0))
+    if (kgwe_flash_attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, work, nullptr, B, S, H, HKV, D, scale, causal, 0))
       std::exit(3);
   };
   hipEvent_t e0, e1;
@@ -81,7 +83,7 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     return ms / n;
   };
-  const double fl = 4.0 * B * H * double(S) * S * D / 2;
+  const double fl = 4.0 * B * H * double(S) * S * D / (causal ? 2 : 1);
   const float tf = timeit(fwd, 30);
   const float tb = timeit(bwd, 20);
   fwd(); bwd();
