@@ -96,6 +96,20 @@ typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 // Accumulator register r of a 32x32 tile holds row (r&3) + 8*(r>>2) + 4*half.
 __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+// Raise a wave's issue priority over its MFMA chains and drop it for the
+// softmax, so each SIMD's arbiter keeps the matrix pipe fed from whichever of
+// its two waves is in an MFMA phase.  Measured (tools/gpu_fa_variants.sh, B=2
+// S=4096 causal): backward 1.142 -> 1.128 ms, forward 0.369 -> 0.384 ms — so
+// on in the dQ and dK/dV kernels, off in the forward.
+#ifndef FA_MFMA_PRIO_FWD
+#define FA_MFMA_PRIO_FWD 0
+#endif
+#ifndef FA_MFMA_PRIO_BWD
+#define FA_MFMA_PRIO_BWD 1
+#endif
+#define FA_PRIO_HI_(on) do { if (on) __builtin_amdgcn_s_setprio(1); } while (0)
+#define FA_PRIO_LO_(on) do { if (on) __builtin_amdgcn_s_setprio(0); } while (0)
+
 // max / sum of lane l and lane l ^ 32 in every lane: one v_permlane32_swap
 // (a VALU half exchange) instead of an LDS ds_bpermute round trip.
 __device__ __forceinline__ float xhalf_max(float x) {
@@ -295,6 +309,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
       // S^T = K Q^T for every sub-block: each K fragment feeds QPW MFMAs.
 #pragma unroll
       for (int j = 0; j < QPW; ++j) sacc[j][0] = sacc[j][1] = f32x16{};
+      FA_PRIO_HI_(FA_MFMA_PRIO_FWD);
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
@@ -303,6 +318,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
 #pragma unroll
           for (int j = 0; j < QPW; ++j) sacc[j][st] = mfma(kf, qf[j][t], sacc[j][st]);
         }
+      FA_PRIO_LO_(FA_MFMA_PRIO_FWD);
     }
     // The other buffers were released by every wave at the last barrier.
     if (more) {
@@ -378,6 +394,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
       // from two hardware-transposed reads of the row-major V tile, at the
       // lane offsets precomputed in voff (+ a compile-time row offset); each
       // V^T fragment feeds QPW MFMAs.
+      FA_PRIO_HI_(FA_MFMA_PRIO_FWD);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int st = s >> 1, sp = s & 1;
@@ -391,6 +408,7 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
           for (int j = 0; j < QPW; ++j) oacc[j][db] = mfma(vf, pk8(pb[j][s]), oacc[j][db]);
         }
       }
+      FA_PRIO_LO_(FA_MFMA_PRIO_FWD);
     }
     if (more) vwrite(cur ^ 1);
     __syncthreads();
@@ -623,20 +641,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
       const bf16_t* Dc = Ds + cur * QTILE;
       const float* Lc = Ls + cur * BQT;
       const float* Dlc = Dl + cur * BQT;
-      // S[q][key] = Q K^T and dP[q][key] = dO V^T (key on the lane).
-      f32x16 sa = f32x16{}, pa = f32x16{};
+      // S[q][key] = Q K^T and dP[q][key] = dO V^T (key on the lane).  The dP
+      // chain starts from -delta (the row constant as the initial
+      // accumulator), so dS = P dP' needs no subtraction.
+      f32x16 sa = f32x16{}, pa;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 del4 = *reinterpret_cast<const f32x4*>(Dlc + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pa[4 * g4 + j] = -del4[j];
+      }
+      FA_PRIO_HI_(FA_MFMA_PRIO_BWD);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         sa = mfma(row_rd(Qc, ao, 0, t), kf[t], sa);
         pa = mfma(row_rd(Dc, ao, 0, t), row_rd(Vmine, ao, 0, t), pa);
       }
+      FA_PRIO_LO_(FA_MFMA_PRIO_BWD);
       // P = exp2(S c - lse2), dS = P (dP - delta); row r <-> query qbase + acc_row(r).
       const bool edge = (causal && key0 + 31 > qbase) || (!EVEN && (qbase + BQT > S || key0 + 32 > S));
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         // accumulator rows 4*g4 .. +3 are queries 8*g4 + 4*hh + 0..3: one b128 read each
         const f32x4 lse4 = *reinterpret_cast<const f32x4*>(Lc + 8 * g4 + 4 * hh);
-        const f32x4 del4 = *reinterpret_cast<const f32x4*>(Dlc + 8 * g4 + 4 * hh);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g4 + j;
@@ -646,7 +673,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
             if ((!EVEN && (key >= S || qrow >= S)) || (causal && key > qrow)) p = 0.f;
           }
           sa[r] = p;
-          pa[r] = p * (pa[r] - del4[j]);
+          pa[r] = p * pa[r];
         }
       }
       // dV^T += dO^T P ; dK^T += Q^T dS   (P, dS as B operands, permuted q order)
@@ -659,11 +686,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
           sw[j] = pk_bf16(pa[8 * s + 2 * j], pa[8 * s + 2 * j + 1]);
         }
         const bf16x8 pb = pk8(pw), sb = pk8(sw);
+        FA_PRIO_HI_(FA_MFMA_PRIO_BWD);
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
           dva[db] = mfma(tr_rd(Dc, ao, 16 * s, db), pb, dva[db]);
           dka[db] = mfma(tr_rd(Qc, ao, 16 * s, db), sb, dka[db]);
         }
+        FA_PRIO_LO_(FA_MFMA_PRIO_BWD);
       }
     }
     if (it + 1 < total) swrite(cur ^ 1);
@@ -814,12 +843,17 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
       // at a time keeps the kernel inside 256 VGPRs.
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        f32x16 sa = f32x16{}, pa = f32x16{};
+        // dP^T starts from -delta (query on the lane: one constant per lane)
+        f32x16 sa = f32x16{}, pa;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pa[r] = -my_delta;
+        FA_PRIO_HI_(FA_MFMA_PRIO_BWD);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           sa = mfma(row_rd(Kc, ao, st * 32, t), qf[t], sa);
           pa = mfma(row_rd(Vc, ao, st * 32, t), df[t], pa);
         }
+        FA_PRIO_LO_(FA_MFMA_PRIO_BWD);
         auto softmax = [&](auto masked) {  // unmasked copy for full tiles (see dK/dV)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -828,7 +862,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
               const int kk = k0 + st * 32 + acc_row(r, hh);
               if ((!EVEN && (kk >= S || qrow >= S)) || (causal && kk > qrow)) p = 0.f;
             }
-            pa[r] = p * (pa[r] - my_delta);  // dS^T
+            pa[r] = p * pa[r];  // dS^T
           }
         };
         if (edge) softmax(std::true_type{});
@@ -840,9 +874,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) sw[j] = pk_bf16(pa[8 * sp + 2 * j], pa[8 * sp + 2 * j + 1]);
           const bf16x8 sb = pk8(sw);
+          FA_PRIO_HI_(FA_MFMA_PRIO_BWD);
 #pragma unroll
           for (int db = 0; db < 4; ++db)
             dqa[db] = mfma(tr_rd(Kc, ao, st * 32 + 16 * sp, db), sb, dqa[db]);
+          FA_PRIO_LO_(FA_MFMA_PRIO_BWD);
         }
       }
     }
