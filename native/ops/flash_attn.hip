@@ -107,8 +107,19 @@ __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (
 #ifndef FA_MFMA_PRIO_BWD
 #define FA_MFMA_PRIO_BWD 1
 #endif
-#define FA_PRIO_HI_(on) do { if (on) __builtin_amdgcn_s_setprio(1); } while (0)
-#define FA_PRIO_LO_(on) do { if (on) __builtin_amdgcn_s_setprio(0); } while (0)
+// mode 1: MFMA chains at priority 1; mode 2: the inverse (softmax phases at
+// priority 1, MFMA chains at 0); mode 3: MFMA chains at priority 3.
+#define FA_PRIO_HI_(on)                                          \
+  do {                                                           \
+    if ((on) == 1) __builtin_amdgcn_s_setprio(1);                \
+    if ((on) == 2) __builtin_amdgcn_s_setprio(0);                \
+    if ((on) == 3) __builtin_amdgcn_s_setprio(3);                \
+  } while (0)
+#define FA_PRIO_LO_(on)                                          \
+  do {                                                           \
+    if ((on) == 1 || (on) == 3) __builtin_amdgcn_s_setprio(0);   \
+    if ((on) == 2) __builtin_amdgcn_s_setprio(1);                \
+  } while (0)
 
 // max / sum of lane l and lane l ^ 32 in every lane: one v_permlane32_swap
 // (a VALU half exchange) instead of an LDS ds_bpermute round trip.
