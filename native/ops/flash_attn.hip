@@ -132,6 +132,30 @@ __device__ __forceinline__ float xhalf_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// Store one row of a transposed accumulator set (acc[db] register r holds
+// column db*32 + acc_row(r, hh) of THIS lane's row), times `mul`, as bf16
+// with 16-B stores: a lane holds 4 consecutive columns per register group,
+// its partner lane (l ^ 32) the next 4, so one v_permlane32_swap per dword
+// pairs them up — 8 global_store_dwordx4 per lane instead of 16 dwordx2
+// (the store-issue-bound epilogue tail, cdna_hip_programming.md T21).  Every
+// lane must execute it (the swaps cross lanes); `ok` guards only the stores.
+__device__ __forceinline__ void store_row_t(bf16_t* row, const f32x16 (&acc)[4], float mul, int hh,
+                                            bool ok) {
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const f32x16& a = acc[db];
+      const int g0 = 4 * (2 * pr), g1 = 4 * (2 * pr + 1);
+      const auto r0 = __builtin_amdgcn_permlane32_swap(pk_bf16(a[g0] * mul, a[g0 + 1] * mul),
+                                                       pk_bf16(a[g1] * mul, a[g1 + 1] * mul), false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(pk_bf16(a[g0 + 2] * mul, a[g0 + 3] * mul),
+                                                       pk_bf16(a[g1 + 2] * mul, a[g1 + 3] * mul), false, false);
+      const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+      if (ok) *reinterpret_cast<u32x4*>(row + db * 32 + 16 * pr + 8 * hh) = v;
+    }
+}
+
 // Decode a 1-D workgroup id into (b, hkv, g, qb): XCD-aware so consecutive
 // logical ids (same kv head) share an XCD; causal: heaviest query blocks first.
 //
@@ -428,18 +452,10 @@ __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
   for (int j = 0; j < QPW; ++j) {
     const int qrow = q0 + 32 * j + lq;
     const float lt = xhalf_sum(l[j]);
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    store_row_t(o + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD, oacc[j],
+                inv, hh, EVEN || qrow < S);
     if (EVEN || qrow < S) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      bf16_t* op = o + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x16& a = oacc[j][db];
-          const u32x2 v2 = {pk_bf16(a[4 * g4] * inv, a[4 * g4 + 1] * inv),
-                            pk_bf16(a[4 * g4 + 2] * inv, a[4 * g4 + 3] * inv)};
-          *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g4 + 4 * hh) = v2;
-        }
       if (hh == 0)
         lse2[(static_cast<size_t>(b) * Hq + h) * S + qrow] = lt > 0.f ? m[j] + log2f(lt) : -INFINITY;
     }
@@ -711,7 +727,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     qt = qt_nxt;
     g_cur = g_nxt;
   }
-  if (slot > 0 && (EVEN || key < S)) {
+  if (slot > 0) {
+    if (!(EVEN || key < S)) return;
     // fp32 partial [slot-1][dk|dv][b][hkv][key][d]
     const size_t plane = static_cast<size_t>(B) * Hkv * S * HD;
     float* pk = part + (static_cast<size_t>(slot - 1) * 2) * plane +
@@ -730,19 +747,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
         *reinterpret_cast<f32x4*>(pk + db * 32 + 8 * g4 + 4 * hh) = a;
         *reinterpret_cast<f32x4*>(pv + db * 32 + 8 * g4 + 4 * hh) = bb;
       }
-  } else if (EVEN || key < S) {
+  } else {
     const size_t off = (static_cast<size_t>(b) * S + key) * kvs + static_cast<size_t>(hkv) * HD;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x16 &ka = dka[db], &va = dva[db];
-        const u32x2 a = {pk_bf16(ka[4 * g4] * scale, ka[4 * g4 + 1] * scale),
-                         pk_bf16(ka[4 * g4 + 2] * scale, ka[4 * g4 + 3] * scale)};
-        const u32x2 bb = {pk_bf16(va[4 * g4], va[4 * g4 + 1]), pk_bf16(va[4 * g4 + 2], va[4 * g4 + 3])};
-        *reinterpret_cast<u32x2*>(dk + off + db * 32 + 8 * g4 + 4 * hh) = a;
-        *reinterpret_cast<u32x2*>(dv + off + db * 32 + 8 * g4 + 4 * hh) = bb;
-      }
+    store_row_t(dk + off, dka, scale, hh, EVEN || key < S);
+    store_row_t(dv + off, dva, 1.f, hh, EVEN || key < S);
   }
 }
 
@@ -896,18 +904,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     if (kt + 1 < ntiles) swrite(cur ^ 1);
     __syncthreads();
   }
-  if (EVEN || qrow < S) {
-    bf16_t* p = dq + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x16& qa = dqa[db];
-        const u32x2 a = {pk_bf16(qa[4 * g4] * scale, qa[4 * g4 + 1] * scale),
-                         pk_bf16(qa[4 * g4 + 2] * scale, qa[4 * g4 + 3] * scale)};
-        *reinterpret_cast<u32x2*>(p + db * 32 + 8 * g4 + 4 * hh) = a;
-      }
-  }
+  store_row_t(dq + (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD, dqa, scale,
+              hh, EVEN || qrow < S);
 }
 
 }  // namespace
