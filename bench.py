@@ -30,7 +30,12 @@ What each rank measures
    build, warmup, timed steps, extra rows) -> ``util_whole_process_pct``.
 3. At N > 1 an FSDP2 row (PyTorch ``fully_shard``) is timed on the same
    shape after the headline row (``--fsdp-row``), and the RCCL all-reduce
-   bus bandwidth over the job's own ranks is swept first.
+   bus bandwidth over the job's own ranks is swept first.  On RCCL the
+   sharded-DP path is also timed for a few steps with the other gradient
+   reduce-scatter dtype (``--reduce-row``: fp32 vs bf16 bytes over xGMI).
+   Before the ranks start, the launcher runs the HIP xGMI peer-pull probe
+   over the N GPUs in a child process of its own (``xgmi_probe``: each link
+   alone, then all links at once).
 Synthetic tokens (a fresh uniform batch every step), random-init weights of
 the Llama-3-8B architecture, bf16 compute, fp32 master weights + AdamW step
 inside every timed step.  Headline data parallelism is kgwe's sharded DP
@@ -81,6 +86,10 @@ def parse(argv=None):
                     help="also time an FSDP2 row after the headline (auto: when N > 1)")
     ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient reduce-scatter dtype of the sharded-DP path at N > 1")
+    ap.add_argument("--reduce-row", default="auto", choices=["auto", "on", "off"],
+                    help="also time the sharded-DP path with the OTHER reduce dtype for a few "
+                         "steps (auto: at N > 1 on RCCL) — what halving the reduce-scatter "
+                         "bytes over xGMI buys")
     ap.add_argument("--in-process", action="store_true",
                     help="run as a single rank in this process (no launcher)")
     return ap.parse_args(argv)
@@ -296,10 +305,42 @@ def rank_main(args) -> int:
     attention = ("sdpa" if (args.sdpa or not attn_ops.hip_flash_available()) else "kgwe_flash_attn")
     tuned = tr.tuned_gemms
 
+    # Reduce-dtype row: the sharded-DP path again with the other gradient
+    # reduce-scatter dtype (fp32 <-> bf16), a few steps, reported beside the
+    # headline.  A failure is reported in the row, never faked.
+    reduce_row = None
+    want_reduce = args.reduce_row == "on" or (args.reduce_row == "auto" and world > 1
+                                              and info.backend == "nccl")
+    if want_reduce and args.parallel == "zero":
+        other = torch.float32 if reduce_dtype == torch.bfloat16 else torch.bfloat16
+        if tr.dp is not None:
+            tr.dp.close()
+        tr = None
+        _release_memory()
+        k2, w2 = min(args.steps, 5), min(args.warmup, 2)
+        try:
+            tr3 = Trainer(TrainConfig(model=args.model, seq_len=args.seq_len,
+                                      micro_batch=args.micro_batch,
+                                      activation_checkpointing=args.ckpt, parallel="zero",
+                                      reduce_dtype=other), info)
+            a3 = argparse.Namespace(**{**vars(args), "steps": k2})
+            r3 = _row(tr3, timed_run(tr3, k2, w2), a3, info, kdist)
+            reduce_row = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r3.items()
+                          if k not in ("losses", "seconds")}
+            reduce_row.update({"grad_reduce_dtype": "bf16" if other == torch.bfloat16 else "fp32",
+                               "steps": k2, "warmup": w2})
+            tr3.dp.close()
+            del tr3
+        except Exception as e:  # noqa: BLE001 - reported, never faked
+            print(f"[bench] rank {info.rank}: reduce-dtype row failed: {e!r}", file=sys.stderr, flush=True)
+            reduce_row = {"error": repr(e)[:300]}
+            tr3 = None
+        _release_memory()
+
     fsdp = None
     want_fsdp = args.fsdp_row == "on" or (args.fsdp_row == "auto" and world > 1)
     if want_fsdp and args.parallel != "fsdp":
-        if tr.dp is not None:
+        if tr is not None and tr.dp is not None:
             tr.dp.close()
         tr = None
         _release_memory()
@@ -365,6 +406,7 @@ def rank_main(args) -> int:
             "attention": attention,
             "gemm_solutions": "tuned (kgwe/tuning)" if tuned else "library default",
             "fsdp_row": fsdp,
+            "reduce_dtype_row": reduce_row,
             "allreduce_busbw_gbps": (round(busbw["peak_busbw_gbps"], 1) if busbw else None),
             "allreduce_sweep": busbw["rows"] if busbw else None,
             "sched": sched,

@@ -49,7 +49,7 @@ def test_bench_gpus4_rehearses_the_multi_rank_path():
     sharded-DP headline row and the FSDP2 row both run and every rank
     reports (the busBW sweep is off: 1 GiB all-reduces on gloo)."""
     r, lines = _run(4, ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1",
-                        "--fsdp-row", "on"], timeout=400)
+                        "--fsdp-row", "on", "--reduce-row", "on"], timeout=400)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(lines[-1])
     assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "zero2-dp4"
@@ -57,6 +57,8 @@ def test_bench_gpus4_rehearses_the_multi_rank_path():
     assert len(out["loss_per_rank"]) == 4 and len(set(out["loss_per_rank"])) == 4
     assert out["fsdp_row"]["parallelism"] == "fsdp4" and "error" not in out["fsdp_row"]
     assert out["config"]["grad_reduce_dtype"] == "fp32"
+    rr = out["reduce_dtype_row"]  # the bf16-reduce row ran (or says why not)
+    assert rr.get("grad_reduce_dtype") == "bf16" or "error" in rr, rr
 
 
 def test_bench_failing_rank_fails_the_launcher():
