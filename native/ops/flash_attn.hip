@@ -1,8 +1,8 @@
 // Causal GQA flash attention for gfx950 (MI355X), bf16 in / fp32 accumulate,
 // head_dim 128, written directly on v_mfma_f32_32x32x16_bf16.
 //
-// Forward (one workgroup = 4 waves = 128 query rows of one (batch, head), two
-// workgroups per CU):
+// Forward (one workgroup = 8 waves = 256 query rows of one (batch, head), one
+// workgroup per CU, two waves per SIMD):
 //   * each wave owns 32 query rows; Q stays in VGPRs for the whole pass
 //     (8 k-steps x bf16x8 = 32 VGPRs);
 //   * K/V tiles of 64 keys are double-buffered in LDS (K row-major with a
@@ -37,9 +37,11 @@
 //     accumulators (no LDS round trip); Q / dO tiles are double-buffered in
 //     ONE swizzled image each, read by rows (ds_read_b128) for S and dP and
 //     by columns (ds_read_b64_tr_b16) for dV^T and dK^T.
-//   * dq kernel: one workgroup = 128 query rows of one (batch, head) (the
-//     forward's geometry, query on the lane): recomputes S^T and dP^T and
-//     accumulates dQ^T += K^T dS^T, K^T read transposed from the K image.
+//   * dq kernel: one workgroup = 8 waves = 256 query rows of one (batch,
+//     head) (the forward's geometry, query on the lane): recomputes S^T and
+//     dP^T and accumulates dQ^T += K^T dS^T, K^T read transposed from the K
+//     image.  8 waves measured ahead of 4 (two workgroups per CU): causal
+//     1.097-1.110 vs 1.119-1.129 ms for the backward, full 1.861 vs 1.914.
 //   * delta = rowsum(dO * O) by a small preprocess kernel.
 #include "common.h"
 
@@ -60,7 +62,14 @@ typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 constexpr int HD = 128;             // head dim
-constexpr int BQ = 128;             // query rows per dQ workgroup
+#ifndef FA_DQ_WAVES
+#define FA_DQ_WAVES 8
+#endif
+constexpr int DQW = FA_DQ_WAVES;    // waves per dQ workgroup (32 query rows each)
+constexpr int BQ = 32 * DQW;        // query rows per dQ workgroup
+constexpr int DQNT = 64 * DQW;      // threads per dQ workgroup
+constexpr int DQSTG = 16 / DQW;     // 16-B K (and V) chunks per thread per 64-key tile
+static_assert(DQW == 4 || DQW == 8, "dQ workgroup: 4 or 8 waves");
 constexpr int BKV = 64;             // keys per forward tile
 constexpr int KST = HD + 8;         // K row stride in LDS (bf16): 272 B
 
@@ -210,7 +219,7 @@ __device__ __forceinline__ u16x4 tr_read(const bf16_t* lds_base, int byte_off) {
 }
 
 #ifndef FA_FWD_WAVES
-#define FA_FWD_WAVES 4
+#define FA_FWD_WAVES 8
 #endif
 #ifndef FA_FWD_QPW
 #define FA_FWD_QPW 1
@@ -227,13 +236,15 @@ static_assert(FNW * QPW <= 8 && 16 % FNW == 0, "at most 256 query rows, 16 stagi
 // K/V tiles of 64 keys double-buffered in LDS (67 KB): the global loads of
 // tile t+1 are issued before tile t's MFMAs and written to the other buffer
 // after them, so one barrier per tile separates the phases.
-// Default geometry, measured with tools/fa_variants.hip (B=2, S=4096, causal,
-// profiles/r01_attn_counters/NOTES.md): 4 waves x 1 sub-block = 128 rows per
-// workgroup, two workgroups per CU (67 KB LDS and <= 256 VGPRs each) —
-// 641 TF/s vs 622 for 8 waves x 1 (one 512-thread workgroup per CU): the two
-// waves sharing a SIMD come from different workgroups, so their barriers do
-// not hold them in lockstep and one wave's softmax overlaps the other's
-// MFMAs.  QPW = 2 (each K / V^T fragment read feeds two MFMAs, one wave per
+// Default geometry, measured with tools/fa_variants.hip (B=2, S=4096):
+// 8 waves x 1 sub-block = 256 rows per workgroup, one 512-thread workgroup
+// per CU (67 KB LDS, <= 256 VGPRs per wave, two waves per SIMD).  In round 1
+// the 4-wave / two-workgroups-per-CU form won (641 vs 622 TF/s,
+// profiles/r01_attn_counters/NOTES.md: barrier coupling of the two waves on
+// a SIMD); after the VALU trims, longest-first dispatch and 16-B epilogue
+// stores, the 8-wave form wins: causal 0.338-0.345 vs 0.354-0.357 ms, full
+// 0.595 vs 0.631 ms (924 TF/s) — each K / V tile staged once feeds twice the
+// rows.  QPW = 2 (each K / V^T fragment read feeds two MFMAs, one wave per
 // SIMD) spills past 256 arch VGPRs and runs at 400-500 TF/s.
 template <bool EVEN>
 __global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
@@ -789,7 +800,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_finalize(const float* __restr
 // layout-(b) images: K rows for S^T = K Q^T and K columns (transposed reads)
 // for dQ^T += K^T dS^T from the same image; V rows for dP^T = V dO^T.
 template <bool EVEN>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
+__global__ __launch_bounds__(DQNT, DQW == 4 ? 2 : 1) void fa_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ delta, bf16_t* __restrict__ dq, int S, int Hq, int Hkv, float c,
@@ -822,21 +833,21 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   const int ntiles = (kv_end + BKV - 1) / BKV;
   const bf16_t* kb_ = k + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
   const bf16_t* vb_ = v + static_cast<size_t>(b) * S * kvs + static_cast<size_t>(hkv) * HD;
-  // Staging: thread t moves chunks (key, ch) = ((t + 256 i) >> 4, t & 15), i = 0..3.
+  // Staging: thread t moves chunks (key, ch) = ((t + DQNT i) >> 4, t & 15), i < DQSTG.
   const int skey = threadIdx.x >> 4, sch = threadIdx.x & 15;
-  bf16x8 kr[4], vr[4];
+  bf16x8 kr[DQSTG], vr[DQSTG];
   auto gload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int s = kt * BKV + skey + 16 * i;
+    for (int i = 0; i < DQSTG; ++i) {
+      const int s = kt * BKV + skey + 4 * DQW * i;
       kr[i] = (EVEN || s < S) ? ld16(kb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
       vr[i] = (EVEN || s < S) ? ld16(vb_ + static_cast<size_t>(s) * kvs + sch * 8) : bf16x8{};
     }
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int off = a_off(skey + 16 * i, sch);
+    for (int i = 0; i < DQSTG; ++i) {
+      const int off = a_off(skey + 4 * DQW * i, sch);
       *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Ks + buf * VTILE) + off) = kr[i];
       *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Vs + buf * VTILE) + off) = vr[i];
     }
@@ -1037,11 +1048,11 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
   rc = KGWE_CHECK_LAUNCH();
   if (rc) return rc;
   if (S % 256 == 0) {
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(DQNT), 0, s,
                        Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
                        nQB);
   } else {
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(256), 0, s,
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(DQNT), 0, s,
                        Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
                        nQB);
   }
