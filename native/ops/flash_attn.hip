@@ -500,6 +500,17 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const bf16_t* __restric
 }
 
 constexpr int BQT = 32;               // query rows per backward step
+// 8 waves (256 keys, one workgroup per CU) measured: full 1.930 -> 1.855 ms
+// for the backward, but causal 1.131 -> 1.144 ms (coarser causal jobs): the
+// training shape is causal, so 4.
+#ifndef FA_DKDV_WAVES
+#define FA_DKDV_WAVES 4
+#endif
+constexpr int KVW = FA_DKDV_WAVES;    // waves per dK/dV workgroup (32 keys each)
+constexpr int KB = 32 * KVW;          // keys per dK/dV workgroup
+constexpr int KVNT = 64 * KVW;        // threads per dK/dV workgroup
+constexpr int QSTG = 8 / KVW;         // 16-B Q (and dO) chunks per thread per 32-row tile
+static_assert(KVW == 4 || KVW == 8, "dK/dV workgroup: 4 or 8 waves");
 constexpr int QTILE = BQT * HD;       // bf16 elements of one Q (or dO) image
 
 // Backward LDS images use layout (a) of cdna_hip_programming.md T10: 8-row x
@@ -555,7 +566,7 @@ __device__ __forceinline__ bf16x8 tr_rd(const bf16_t* img, const AOffs& o, int b
 // SIMD) — over it, hipcc parks the excess in AGPRs and moves it back and forth
 // every iteration.  K stays in VGPRs, the WG's V tile is read from LDS.
 template <bool EVEN>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
+__global__ __launch_bounds__(KVNT, KVW == 4 ? 2 : 1) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ delta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S,
@@ -563,7 +574,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     float* __restrict__ part, int B) {
   __shared__ __attribute__((aligned(16))) bf16_t Qs[2 * QTILE];
   __shared__ __attribute__((aligned(16))) bf16_t Ds[2 * QTILE];
-  __shared__ __attribute__((aligned(16))) bf16_t Vw[128 * HD];  // this WG's 128 keys
+  __shared__ __attribute__((aligned(16))) bf16_t Vw[KB * HD];  // this WG's KB keys
   __shared__ __attribute__((aligned(16))) float Ls[2 * BQT];
   __shared__ __attribute__((aligned(16))) float Dl[2 * BQT];
   const int G = Hq / Hkv;
@@ -589,11 +600,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     b = wg / (nKB * Hkv);
     slot = 0;
     it0 = 0;
-    it1 = G * (nqt - (causal ? (kb * 128) / BQT : 0));
+    it1 = G * (nqt - (causal ? (kb * KB) / BQT : 0));
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lk = lane & 31, hh = lane >> 5;
-  const int key0 = kb * 128 + w * 32;
+  const int key0 = kb * KB + w * 32;
   const int key = key0 + lk;
   const size_t qs = static_cast<size_t>(Hq) * HD, kvs = static_cast<size_t>(Hkv) * HD;
   bf16x8 kf[8];
@@ -605,7 +616,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
     // by the barrier before the main loop.
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int r = (threadIdx.x >> 4) + 16 * i, ch = threadIdx.x & 15, s = kb * 128 + r;
+      const int r = (threadIdx.x >> 4) + 4 * KVW * i, ch = threadIdx.x & 15, s = kb * KB + r;
       const bf16x8 x = (EVEN || s < S) ? ld16(v + (static_cast<size_t>(b) * S + s) * kvs +
                                     static_cast<size_t>(hkv) * HD + ch * 8)
                              : bf16x8{};
@@ -618,17 +629,17 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   for (int i = 0; i < 4; ++i) dka[i] = dva[i] = f32x16{};
 
   const int total = it1 - it0;
-  // Staging: thread t moves row chunks (r, ch) = ((t + 256 i) >> 4, t & 15), i = 0, 1.
+  // Staging: thread t moves row chunks (r, ch) = ((t + KVNT i) >> 4, t & 15), i < QSTG.
   const int sr = threadIdx.x >> 4, sch = threadIdx.x & 15;
-  bf16x8 qr[2], dr[2];
+  bf16x8 qr[QSTG], dr[QSTG];
   float lr = 0.f, drl = 0.f;
   // Iteration it = (query tile nqt-1 - it/G, head g = it%G), tracked
   // incrementally (G is a runtime value: no per-iteration integer division).
   auto gload = [&](int g, int qt) {
     const int h = hkv * G + g;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int s = qt * BQT + sr + 16 * i;
+    for (int i = 0; i < QSTG; ++i) {
+      const int s = qt * BQT + sr + 4 * KVW * i;
       const size_t off = (static_cast<size_t>(b) * S + s) * qs + static_cast<size_t>(h) * HD + sch * 8;
       qr[i] = (EVEN || s < S) ? ld16(q + off) : bf16x8{};
       dr[i] = (EVEN || s < S) ? ld16(dout + off) : bf16x8{};
@@ -642,8 +653,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(
   };
   auto swrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int off = a_off(sr + 16 * i, sch);
+    for (int i = 0; i < QSTG; ++i) {
+      const int off = a_off(sr + 4 * KVW * i, sch);
       *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Qs + buf * QTILE) + off) = qr[i];
       *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(Ds + buf * QTILE) + off) = dr[i];
     }
@@ -941,13 +952,13 @@ struct BwdPlan {
 
 BwdPlan make_plan(int B, int S, int Hq, int Hkv, int causal, int num_cus) {
   BwdPlan p;
-  constexpr int kblk = 128;  // keys per fa_bwd_dkdv_kernel workgroup
+  constexpr int kblk = KB;  // keys per fa_bwd_dkdv_kernel workgroup
   const int G = Hq / Hkv, nqt = (S + BQT - 1) / BQT, nKB = (S + kblk - 1) / kblk;
   const int groups = B * Hkv;
   auto work = [&](int kb) { return G * (nqt - (causal ? (kb * kblk) / BQT : 0)); };
   double total = 0;
   for (int kb = 0; kb < nKB; ++kb) total += static_cast<double>(work(kb)) * groups;
-  const double avg = total / (2.0 * num_cus);  // two dK/dV workgroups per CU
+  const double avg = total / ((KVW == 4 ? 2.0 : 1.0) * num_cus);  // dK/dV workgroups per CU
   struct J { int4 j; int w; };
   std::vector<std::vector<J>> per_xcd(8);
   int nsplit = 0;
@@ -1025,7 +1036,7 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
                      static_cast<const bf16_t*>(o), static_cast<const bf16_t*>(dout), work, B, S, Hq);
   int rc = KGWE_CHECK_LAUNCH();
   if (rc) return rc;
-  const int nKB = (S + 127) / 128;
+  const int nKB = (S + KB - 1) / KB;
   const int nQB = (S + BQ - 1) / BQ;
   const bf16_t *Q = static_cast<const bf16_t*>(q), *Kp = static_cast<const bf16_t*>(k),
                *V = static_cast<const bf16_t*>(v), *DO = static_cast<const bf16_t*>(dout);
@@ -1037,11 +1048,11 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
   const unsigned dkdv_grid = plan ? static_cast<unsigned>(plan->grid) : static_cast<unsigned>(B * Hkv * nKB);
   // EVEN: every tile is full (no per-row bounds checks in the inner loops).
   if (S % 256 == 0) {
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, dim3(dkdv_grid), dim3(256), 0,
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<true>, dim3(dkdv_grid), dim3(KVNT), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
                        S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
   } else {
-    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(dkdv_grid), dim3(256), 0,
+    hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(dkdv_grid), dim3(KVNT), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
                        S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
   }
