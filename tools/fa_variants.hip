@@ -37,7 +37,8 @@ static float b2f(unsigned short b) {
 int main(int argc, char** argv) {
   const char* tag = argc > 1 ? argv[1] : "base";
   const char* ref = argc > 2 ? argv[2] : nullptr;  // baseline dump to compare against
-  const int B = 2, S = 4096, H = 32, HKV = 8, D = 128;
+  // FA_B in the environment sets the batch (the training step runs B=4)
+  const int B = std::getenv("FA_B") ? std::atoi(std::getenv("FA_B")) : 2, S = 4096, H = 32, HKV = 8, D = 128;
   const size_t nq = size_t(B) * S * H * D, nkv = size_t(B) * S * HKV * D;
   std::vector<unsigned short> hq(nq), hk(nkv), hv(nkv), hdo(nq);
   unsigned long long st = 12345;
