@@ -247,7 +247,7 @@ static_assert(FNW * QPW <= 8 && 16 % FNW == 0, "at most 256 query rows, 16 stagi
 // rows.  QPW = 2 (each K / V^T fragment read feeds two MFMAs, one wave per
 // SIMD) spills past 256 arch VGPRs and runs at 400-500 TF/s.
 template <bool EVEN>
-__global__ __launch_bounds__(FNT, QPW == 1 ? 2 : 1) void fa_fwd_kernel(
+__global__ __launch_bounds__(FNT, (QPW == 1 && FNW <= 4) ? 2 : 1) void fa_fwd_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     bf16_t* __restrict__ o, float* __restrict__ lse2, int S, int Hq, int Hkv, float c,
     int causal, int nQB) {
