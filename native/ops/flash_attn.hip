@@ -261,7 +261,11 @@ __global__ __launch_bounds__(FNT, (QPW == 1 && FNW <= 4) ? 2 : 1) void fa_fwd_ke
   const size_t qs = static_cast<size_t>(Hq) * HD, kvs = static_cast<size_t>(Hkv) * HD;
   // 8 waves: the second-dispatched half loses VALU arbitration on every
   // segment; one static priority bump evens it out (MI355X_MICROARCH.md).
-  if (FNW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#ifndef FA_FWD_HALF_PRIO
+#define FA_FWD_HALF_PRIO 1
+#endif
+  if (FA_FWD_HALF_PRIO && FNW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
+    __builtin_amdgcn_s_setprio(1);
 
   bf16x8 qf[QPW][8];
 #pragma unroll

@@ -4,7 +4,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from kgwe.ops import attn
 
-B, S, H, HKV, D = 2, 4096, 32, 8, 128
+B = int(os.environ.get("FA_B", "2"))
+S, H, HKV, D = 4096, 32, 8, 128
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn(B, S, h, D, device="cuda", dtype=torch.bfloat16, generator=g).requires_grad_(True)
            for h in (H, HKV, HKV))
