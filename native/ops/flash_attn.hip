@@ -218,6 +218,14 @@ __device__ __forceinline__ u16x4 tr_read(const bf16_t* lds_base, int byte_off) {
   return __builtin_bit_cast(u16x4, r);
 }
 
+// Deferred running max (cdna_hip_programming.md T13) with a 2^4 bound on P:
+// at B=4, S=4096 causal the forward goes 0.672-0.684 -> 0.650-0.654 ms; the
+// numerics cases (growing max, a x6 max jump mid-sweep) stay within one bf16
+// ulp of the fp32 reference (tools/fa_fwd_err.py: max 1.56e-2 at |O| ~ 2-4).
+// T = 8 had failed the max-jump case at 2 ulps (round-2 session 1).
+#ifndef FA_DEFER_T
+#define FA_DEFER_T 4.f
+#endif
 #ifndef FA_FWD_WAVES
 #define FA_FWD_WAVES 8
 #endif
@@ -403,14 +411,16 @@ __global__ __launch_bounds__(FNT, (QPW == 1 && FNW <= 4) ? 2 : 1) void fa_fwd_ke
             for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[j][st][r]);
         }
         mx = xhalf_max(mx) * c;
-        const float m_new = fmaxf(m[j], mx);
+        // FA_DEFER_T > 0: keep the running max until a tile's max exceeds it
+        // by more than T (log2 units), so P stays <= 2^T and O is rescaled on
+        // far fewer tiles (any of the wave's 32 rows moving triggers it).
+        const float m_new = (FA_DEFER_T <= 0.f || mx > m[j] + FA_DEFER_T) ? fmaxf(m[j], mx) : m[j];
         m_use[j] = m_new == -INFINITY ? 0.f : m_new;
         moved |= m_new > m[j];
         alpha[j] = fast_exp2(m[j] - m_use[j]);
         m[j] = m_new;
       }
-      // Rescale O only when some row's max moved (exact; after the first few
-      // tiles the running max rarely changes).
+      // Rescale O only when some row's (deferred) max moved.
       if (__any(moved)) {
 #pragma unroll
         for (int j = 0; j < QPW; ++j) {
