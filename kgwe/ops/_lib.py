@@ -17,7 +17,9 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / "libkgwe_ops.so"
+# KGWE_OPS_LIB: load another build of the kernels (same-box A/B runs only).
+_LIB_PATH = (Path(os.environ["KGWE_OPS_LIB"]) if os.environ.get("KGWE_OPS_LIB")
+             else Path(__file__).resolve().parent.parent / "_lib" / "libkgwe_ops.so")
 _lib = None
 
 c_void_p = ctypes.c_void_p
