@@ -8,7 +8,5 @@ mkdir -p fa_var_bin
 rm -f fa_var_bin/fa_*
 b() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 "${@:2}" tools/fa_variants.hip -o fa_var_bin/fa_$1; }
 b base -fno-slp-vectorize &
-b t1 -fno-slp-vectorize -DFA_DEFER_T=1.f &
-b t2 -fno-slp-vectorize -DFA_DEFER_T=2.f &
-b t4 -fno-slp-vectorize -DFA_DEFER_T=4.f &
+b w4 -fno-slp-vectorize -DFA_FWD_WAVES=4 &
 wait
