@@ -62,6 +62,9 @@ typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 constexpr int HD = 128;             // head dim
+#ifndef FA_DQ_DELTA
+#define FA_DQ_DELTA 1
+#endif
 #ifndef FA_DQ_WAVES
 #define FA_DQ_WAVES 8
 #endif
@@ -827,8 +830,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_finalize(const float* __restr
 template <bool EVEN>
 __global__ __launch_bounds__(DQNT, DQW == 4 ? 2 : 1) void fa_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
-    const float* __restrict__ delta, bf16_t* __restrict__ dq, int S, int Hq, int Hkv, float c,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const bf16_t* __restrict__ o,
+    float* __restrict__ delta, bf16_t* __restrict__ dq, int S, int Hq, int Hkv, float c,
     float scale, int causal, int nQB) {
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2 * VTILE];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2 * VTILE];
@@ -840,6 +843,7 @@ __global__ __launch_bounds__(DQNT, DQW == 4 ? 2 : 1) void fa_bwd_dq_kernel(
   const int qrow = q0 + lq;
   const size_t qs = static_cast<size_t>(Hq) * HD, kvs = static_cast<size_t>(Hkv) * HD;
   bf16x8 qf[8], df[8];
+  float dsum = 0.f;
   {
     const size_t off = (static_cast<size_t>(b) * S + qrow) * qs + static_cast<size_t>(h) * HD;
 #pragma unroll
@@ -847,10 +851,27 @@ __global__ __launch_bounds__(DQNT, DQW == 4 ? 2 : 1) void fa_bwd_dq_kernel(
       qf[t] = (EVEN || qrow < S) ? ld16(q + off + 16 * t + 8 * hh) : bf16x8{};
       df[t] = (EVEN || qrow < S) ? ld16(dout + off + 16 * t + 8 * hh) : bf16x8{};
     }
+    if (FA_DQ_DELTA) {
+      // delta = rowsum(dO * O) for this lane's row, computed here (each lane
+      // pair holds the row's dO already) instead of by a separate pass; the
+      // dK/dV kernel, launched after this one, reads it back.
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const bf16x8 ov = (EVEN || qrow < S) ? ld16(o + off + 16 * t + 8 * hh) : bf16x8{};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsum = fmaf(bf2f(df[t][e]), bf2f(ov[e]), dsum);
+      }
+    }
   }
   const size_t li = (static_cast<size_t>(b) * Hq + h) * S + qrow;
   const float my_lse = (EVEN || qrow < S) ? lse2[li] : INFINITY;
-  const float my_delta = (EVEN || qrow < S) ? delta[li] : 0.f;
+  float my_delta;
+  if (FA_DQ_DELTA) {
+    my_delta = xhalf_sum(dsum);
+    if (hh == 0 && (EVEN || qrow < S)) delta[li] = my_delta;
+  } else {
+    my_delta = (EVEN || qrow < S) ? delta[li] : 0.f;
+  }
   f32x16 dqa[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) dqa[i] = f32x16{};
@@ -1046,14 +1067,31 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
   if (D != HD || Hq % Hkv != 0 || B <= 0 || S <= 0) return -1;
   const float c = scale * 1.4426950408889634f;
   const long long rows = static_cast<long long>(B) * S * Hq;
-  hipLaunchKernelGGL(fa_bwd_pre_kernel, dim3(static_cast<unsigned>((rows * 16 + 255) / 256)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(o), static_cast<const bf16_t*>(dout), work, B, S, Hq);
-  int rc = KGWE_CHECK_LAUNCH();
-  if (rc) return rc;
+  int rc = 0;
+  if (!FA_DQ_DELTA) {
+    hipLaunchKernelGGL(fa_bwd_pre_kernel, dim3(static_cast<unsigned>((rows * 16 + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(o), static_cast<const bf16_t*>(dout), work, B, S, Hq);
+    rc = KGWE_CHECK_LAUNCH();
+    if (rc) return rc;
+  }
   const int nKB = (S + KB - 1) / KB;
   const int nQB = (S + BQ - 1) / BQ;
   const bf16_t *Q = static_cast<const bf16_t*>(q), *Kp = static_cast<const bf16_t*>(k),
-               *V = static_cast<const bf16_t*>(v), *DO = static_cast<const bf16_t*>(dout);
+               *V = static_cast<const bf16_t*>(v), *DO = static_cast<const bf16_t*>(dout),
+               *O = static_cast<const bf16_t*>(o);
+  // dQ first: with FA_DQ_DELTA it also writes delta = rowsum(dO * O), which
+  // the dK/dV kernel reads.
+  if (S % 256 == 0) {
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(DQNT), 0, s,
+                       Q, Kp, V, DO, lse2, O, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
+                       nQB);
+  } else {
+    hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(DQNT), 0, s,
+                       Q, Kp, V, DO, lse2, O, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
+                       nQB);
+  }
+  rc = KGWE_CHECK_LAUNCH();
+  if (rc) return rc;
   // Planned dK/dV jobs (balanced causal sweep); the analytic one-block-per-
   // workgroup grid when no plan can be built (first call inside a capture).
   const BwdPlan* plan = get_plan(B, S, Hq, Hkv, causal, s);  // null: analytic grid
@@ -1069,17 +1107,6 @@ KGWE_API int kgwe_flash_attn_bwd(const void* q, const void* k, const void* v, co
     hipLaunchKernelGGL(fa_bwd_dkdv_kernel<false>, dim3(dkdv_grid), dim3(KVNT), 0,
                        s, Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dk), static_cast<bf16_t*>(dv),
                        S, Hq, Hkv, c, scale, causal, nKB, jobs, part, B);
-  }
-  rc = KGWE_CHECK_LAUNCH();
-  if (rc) return rc;
-  if (S % 256 == 0) {
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<true>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(DQNT), 0, s,
-                       Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
-                       nQB);
-  } else {
-    hipLaunchKernelGGL(fa_bwd_dq_kernel<false>, dim3(static_cast<unsigned>(B * Hq * nQB)), dim3(DQNT), 0, s,
-                       Q, Kp, V, DO, lse2, work, static_cast<bf16_t*>(dq), S, Hq, Hkv, c, scale, causal,
-                       nQB);
   }
   rc = KGWE_CHECK_LAUNCH();
   if (rc) return rc;

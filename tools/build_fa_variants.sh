@@ -8,5 +8,5 @@ mkdir -p fa_var_bin
 rm -f fa_var_bin/fa_*
 b() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 "${@:2}" tools/fa_variants.hip -o fa_var_bin/fa_$1; }
 b base -fno-slp-vectorize &
-b w4 -fno-slp-vectorize -DFA_FWD_WAVES=4 &
+b nofuse -fno-slp-vectorize -DFA_DQ_DELTA=0 &
 wait
