@@ -95,17 +95,36 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     for (int j = 0; j < 8; ++j) dw[i][j] = 0.f;
   const float invH = 1.f / static_cast<float>(H);
   int parity = 0;
+  // Rows are software-pipelined: the next row's dy / h (and this row's
+  // residual gradient) are issued before the row's block reduction, so their
+  // latency hides behind the barrier and the output pass instead of opening
+  // each row: 114 -> 108.5 us at T=16384, H=4096 (tools/rmsnorm_ab.hip).
+  bf16x8 d[NW], hv[NW];
+  if (active && static_cast<int>(blockIdx.x) < T) {
+    const size_t base0 = static_cast<size_t>(blockIdx.x) * H;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int col = ((i * 4 + wid) * kWave + lane) * 8;
+      d[i] = *reinterpret_cast<const bf16x8*>(dy + base0 + col);
+      hv[i] = *reinterpret_cast<const bf16x8*>(h + base0 + col);
+    }
+  }
   for (int row = blockIdx.x; row < T; row += gridDim.x, parity ^= 1) {
     const size_t base = static_cast<size_t>(row) * H;
     const float rstd = rstd_in[row];
-    bf16x8 d[NW], hv[NW];
+    const int nrow = row + gridDim.x;
+    const size_t nbase = static_cast<size_t>(nrow) * H;
+    bf16x8 dn[NW], hn[NW], av[NW];
     float dot = 0.f;
     if (active) {
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
         const int col = ((i * 4 + wid) * kWave + lane) * 8;
-        d[i] = *reinterpret_cast<const bf16x8*>(dy + base + col);
-        hv[i] = *reinterpret_cast<const bf16x8*>(h + base + col);
+        if (dadd) av[i] = *reinterpret_cast<const bf16x8*>(dadd + base + col);
+        if (nrow < T) {
+          dn[i] = *reinterpret_cast<const bf16x8*>(dy + nbase + col);
+          hn[i] = *reinterpret_cast<const bf16x8*>(h + nbase + col);
+        }
       }
 #pragma unroll
       for (int i = 0; i < NW; ++i) {
@@ -130,14 +149,14 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
         const float df = bf2f(d[i][j]), hf = bf2f(hv[i][j]);
         dw[i][j] += df * hf * rstd;
         o[j] = rstd * (df * bf2f(wv[j]) - hf * c);
-      }
-      if (dadd) {
-        float a[8];
-        load8(dadd + base + col, a);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] += a[j];
+        if (dadd) o[j] += bf2f(av[i][j]);
       }
       store8(dx + base + col, o);
+    }
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      d[i] = dn[i];
+      hv[i] = hn[i];
     }
   }
   // Stage the workgroup's dw row in LDS, then add it with atomics whose 64
