@@ -37,6 +37,11 @@ HIP_FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
     "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
     "-munsafe-fp-atomics",
+    # No packed-FP32 VALU forms (v_pk_add/mul/fma_f32): hipcc -O3 otherwise
+    # forms them from ordinary float code, and some of their forms have given
+    # silently wrong results on this GPU pool.  (The host pass warns that it
+    # does not know the feature; harmless.)
+    "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
 ]
 # Per-source extras.  flash_attn.hip: no SLP vectorisation — hipcc otherwise
 # packs the softmax's adjacent f32 adds / multiplies into v_pk_*_f32, which

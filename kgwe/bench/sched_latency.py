@@ -180,8 +180,13 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
     slice_util: list[float] = []
     queue_depth: list[int] = []
 
+    _no = os.environ.get("KGWE_BENCH_NO", "")
+
     def partition_sampler():  # time-average of CPX/QPX/DPX slice occupancy
         while not done.is_set():
+            if "sampler" in _no:
+                time.sleep(0.1)
+                continue
             m = plat.partition_metrics()
             if any(k != "SPX" and v.get("gpus", 0) for k, v in m.get("modes", {}).items()):
                 slice_util.append(m.get("slice_utilization", 0.0))
@@ -189,8 +194,10 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
 
     def housekeeping():
         while not done.is_set():
-            plat.tick()
-            plat.consolidate_partitions(plan_only=False)  # the controller's consolidation (ledger move)
+            if "tick" not in _no:
+                plat.tick()
+            if "consolidate" not in _no:
+                plat.consolidate_partitions(plan_only=False)  # the controller's consolidation (ledger move)
             queue_depth.append(plat.queue_depth())
             time.sleep(tick_s)
 
@@ -225,7 +232,8 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
                                                     if slice_util else None),
                 "partition_slice_samples": len(slice_util),
                 "topology_optimal_placements": sm.get("topology_optimal", 0),
-                "extender_phases_ms": ext.tracer.summary(),
+                "extender_phases_ms": ext.phase_summary(),
+                "extender_server": {k: v for k, v in ext.stats().items() if k != "verbs"},
             })
             ext.stop()
             return

@@ -10,6 +10,7 @@
 #include "extender_scan.h"
 #include "hal.h"
 #include "histogram.h"
+#include "http_server.h"
 #include "platform.h"
 
 namespace py = pybind11;
@@ -92,6 +93,84 @@ struct PyPlatform {
     auto it = fakes.find(node);
     if (it == fakes.end()) throw std::runtime_error("no fake HAL for node " + node);
     return *it->second;
+  }
+};
+
+// The native extender server with its Python-side hooks.  Hooks run on the
+// server's worker threads: each takes the GIL for the call only.
+struct PyHttpServer {
+  std::shared_ptr<ExtenderHttpServer> srv;
+  // Hook objects are shared with the server's std::functions and must die
+  // under the GIL.
+  struct Hook {
+    py::object fn;
+    ~Hook() {
+      py::gil_scoped_acquire g;
+      fn = py::object();
+    }
+  };
+
+  PyHttpServer(PyPlatform& p, const std::string& host, int port, const std::string& prefix, int workers,
+               int gang_hold_ms) {
+    ExtenderHttpServer::Options o;
+    o.host = host;
+    o.port = port;
+    o.prefix = prefix;
+    o.workers = workers;
+    o.gang_hold_ms = gang_hold_ms;
+    srv = std::make_shared<ExtenderHttpServer>(p.p, o);
+  }
+
+  void set_bind_sink(py::object fn) {
+    auto h = std::make_shared<Hook>();
+    h->fn = std::move(fn);
+    srv->set_bind_sink([h](const std::string& args, const std::string& result) {
+      py::gil_scoped_acquire g;
+      try {
+        return h->fn(py::bytes(args), py::bytes(result)).cast<std::string>();
+      } catch (py::error_already_set& e) {
+        std::string what = e.what();
+        e.restore();
+        PyErr_Clear();
+        return what.empty() ? std::string("bind sink failed") : what;
+      }
+    });
+  }
+
+  void set_pod_lookup(py::object fn) {
+    auto h = std::make_shared<Hook>();
+    h->fn = std::move(fn);
+    srv->set_pod_lookup([h](const std::string& ns, const std::string& name) {
+      py::gil_scoped_acquire g;
+      try {
+        return h->fn(ns, name).cast<std::string>();
+      } catch (py::error_already_set& e) {
+        e.restore();
+        PyErr_Clear();
+        return std::string();
+      }
+    });
+  }
+
+  void set_fallback(py::object fn) {
+    auto h = std::make_shared<Hook>();
+    h->fn = std::move(fn);
+    srv->set_fallback([h](const HttpRequest& rq) {
+      HttpResponse r;
+      py::gil_scoped_acquire g;
+      try {
+        py::tuple t = h->fn(rq.method, rq.path, py::bytes(rq.body)).cast<py::tuple>();
+        r.code = t[0].cast<int>();
+        r.body = t[1].cast<std::string>();
+        if (t.size() > 2) r.ctype = t[2].cast<std::string>();
+      } catch (py::error_already_set& e) {
+        r.code = 500;
+        r.body = std::string("{\"error\":\"") + json_escape(e.what()) + "\"}";
+        e.restore();
+        PyErr_Clear();
+      }
+      return r;
+    });
   }
 };
 
@@ -484,4 +563,23 @@ PYBIND11_MODULE(_kgwe_core, m) {
         return s.p->metrics()->value(name, labels);
       }, py::call_guard<py::gil_scoped_release>())
       .def("metric_families", [](PyPlatform& s) { return s.p->metrics()->families(); }, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<PyHttpServer>(m, "HttpServer")
+      .def(py::init<PyPlatform&, const std::string&, int, const std::string&, int, int>(), py::arg("platform"),
+           py::arg("host") = "0.0.0.0", py::arg("port") = 8080, py::arg("prefix") = "", py::arg("workers") = 0,
+           py::arg("gang_hold_ms") = 25000)
+      .def("start", [](PyHttpServer& s) {
+        const std::string err = s.srv->start();
+        if (!err.empty()) throw std::runtime_error(err);
+      }, py::call_guard<py::gil_scoped_release>())
+      .def("stop", [](PyHttpServer& s) { s.srv->stop(); }, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", [](PyHttpServer& s) { return s.srv->port(); })
+      .def("set_ready", [](PyHttpServer& s, bool r) { s.srv->set_ready(r); })
+      .def("set_verbs_via_fallback", [](PyHttpServer& s, bool v) { s.srv->set_verbs_via_fallback(v); })
+      .def("set_bind_sink", &PyHttpServer::set_bind_sink)
+      .def("set_pod_lookup", &PyHttpServer::set_pod_lookup)
+      .def("set_fallback", &PyHttpServer::set_fallback)
+      .def("parked", [](PyHttpServer& s) { return s.srv->parked(); })
+      .def("stats_json", [](PyHttpServer& s) { return s.srv->stats_json(); },
+           py::call_guard<py::gil_scoped_release>());
 }

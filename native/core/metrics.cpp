@@ -94,6 +94,7 @@ void MetricRegistry::clear(const std::string& name) {
   Family* f = find(name);
   f->series.clear();
   f->frozen.reset();
+  f->blocks.reset();
 }
 
 double MetricRegistry::value(const std::string& name, const Labels& lv) const {
@@ -102,7 +103,13 @@ double MetricRegistry::value(const std::string& name, const Labels& lv) const {
   if (it == fams_.end()) return 0.0;
   const SeriesMap& m = it->second.frozen ? *it->second.frozen : it->second.series;
   auto s = m.find(lv);
-  if (s == m.end()) return 0.0;
+  if (s == m.end()) {
+    if (it->second.blocks)
+      for (const auto& b : *it->second.blocks)
+        for (const auto& e : *b.second)
+          if (e.first == lv) return e.second;
+    return 0.0;
+  }
   return it->second.type == MetricType::Histogram ? static_cast<double>(s->second.count) : s->second.value;
 }
 
@@ -141,6 +148,16 @@ void MetricRegistry::commit(GaugeBatch&& batch) {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& kv : batch.fams_) arity.push_back(find(kv.first)->labels.size());
   }
+  for (const auto& kv : batch.blocks_) {  // arity of block series, checked off the lock
+    size_t want = 0;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      want = find(kv.first)->labels.size();
+    }
+    for (const auto& b : kv.second)
+      for (const auto& e : *b.second)
+        if (e.first.size() != want) throw std::runtime_error("label arity mismatch for " + kv.first);
+  }
   std::vector<std::pair<std::string, std::shared_ptr<const SeriesMap>>> staged;
   staged.reserve(batch.fams_.size());
   size_t i = 0;
@@ -163,6 +180,9 @@ void MetricRegistry::commit(GaugeBatch&& batch) {
       Family* f = find(st.first);
       f->frozen.swap(st.second);  // old snapshot freed below, off the lock
       f->series.clear();
+      auto bi = batch.blocks_.find(st.first);
+      if (bi != batch.blocks_.end()) f->blocks = std::make_shared<const BlockMap>(std::move(bi->second));
+      else f->blocks.reset();
     }
   }
 }
@@ -181,6 +201,10 @@ std::string MetricRegistry::expose() const {
                                                                                             : "histogram";
     out += "# HELP " + kv.first + " " + f.help + "\n";
     out += "# TYPE " + kv.first + " " + t + "\n";
+    if (f.blocks)
+      for (const auto& b : *f.blocks)
+        for (const auto& e : *b.second)
+          out += kv.first + label_str(f.labels, e.first) + " " + prom_number(e.second) + "\n";
     for (const auto& s : series) {
       if (f.type != MetricType::Histogram) {
         out += kv.first + label_str(f.labels, s.first) + " " + prom_number(s.second.value) + "\n";

@@ -54,6 +54,16 @@ class MetricRegistry {
     uint64_t count = 0;
   };
   using SeriesMap = std::map<Labels, Series>;
+
+ public:
+  // Gauge series grouped in immutable blocks (one per source object, e.g. a
+  // node): a refresh re-uses the block of every source that did not change,
+  // so its cost — and its allocator churn — follows the changes, not the
+  // fleet size.
+  using Block = std::vector<std::pair<Labels, double>>;
+  using BlockMap = std::map<std::string, std::shared_ptr<const Block>>;
+
+ private:
   struct Family {
     MetricType type;
     std::string help;
@@ -64,6 +74,7 @@ class MetricRegistry {
     // so expose() copies a pointer under the lock, not 10^5 series.  A later
     // set()/add() on the family copies it back into `series` (copy-on-write).
     std::shared_ptr<const SeriesMap> frozen;
+    std::shared_ptr<const BlockMap> blocks;  // committed gauge blocks, beside `frozen`
   };
   Family* find(const std::string& name);
   Family* find_mut(const std::string& name);  // find + thaw a committed family
@@ -78,10 +89,16 @@ class GaugeBatch {
   void set(const std::string& name, MetricRegistry::Labels lv, double v) { fams_[name][std::move(lv)] = v; }
   void add(const std::string& name, MetricRegistry::Labels lv, double v) { fams_[name][std::move(lv)] += v; }
   void touch(const std::string& name) { fams_[name]; }  // replace even when it ends up empty
+  // Series of `name` that come as one shared block per source `key`.
+  void block(const std::string& name, const std::string& key, std::shared_ptr<const MetricRegistry::Block> b) {
+    fams_[name];
+    blocks_[name][key] = std::move(b);
+  }
 
  private:
   friend class MetricRegistry;
   std::map<std::string, std::map<MetricRegistry::Labels, double>> fams_;
+  std::map<std::string, MetricRegistry::BlockMap> blocks_;
 };
 
 std::string prom_escape(const std::string& v);

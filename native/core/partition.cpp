@@ -185,7 +185,7 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
     if (!valid_mode_combo(to, op.mem_to)) {
       op.state = OpState::Failed;
       op.error = std::string("invalid mode combination ") + to_string(to) + "/" + to_string(op.mem_to);
-    } else if (!gpu_idle(g) || (fenced && !sched_->fence_gpu(g.uuid))) {
+    } else if (!gpu_idle(g) || (fenced && !sched_->fence_gpu(g.uuid, node))) {
       op.state = OpState::Failed;
       op.error = "gpu no longer idle";
     } else if (dry_run_) {
@@ -209,7 +209,7 @@ PartitionOp PartitionController::execute(const std::string& node, const GpuDevic
         op.state = OpState::Failed;
         op.error = err;
       }
-      if (fenced) sched_->unfence_gpu(g.uuid);
+      if (fenced) sched_->unfence_gpu(g.uuid, node);
     }
     op.finished_ns = now_ns();
   }
@@ -225,41 +225,71 @@ std::vector<PartitionOp> PartitionController::ensure_capacity(ComputePartition m
   std::vector<PartitionOp> out;
   if (memory && !valid_mode_combo(mode, *memory)) return out;
   auto snap = disc_->snapshot();
-  int have = free_slices(*snap, mode, memory, within);
+  // One memoised ledger summary per node (idle GPUs, free slices) instead of
+  // a ledger probe per GPU: this runs inside the extender's filter verb.
+  struct Cand {
+    const std::string* node;
+    const GpuDevice* g;
+    int node_has_mode, node_idle;
+    size_t seq;  // discovery order: the tie-break that keeps the choice deterministic
+  };
+  std::vector<Cand> cands;
+  int have = 0;
+  for (const auto& kv : snap->nodes) {
+    if (within && !within->count(kv.first)) continue;
+    const NodeTopology& n = kv.second;
+    Scheduler::NodeSummary sum;
+    if (sched_) {
+      sum = sched_->node_summary(n);
+    } else {
+      sum.free_slices.assign(n.gpus.size(), 0);
+      for (size_t p = 0; p < n.gpus.size(); ++p) {
+        if (gpu_idle(n.gpus[p]) && p < 64) sum.idle_mask |= 1ull << p;
+        for (const auto& pi : n.gpus[p].partition.instances) sum.free_slices[p] += pi.in_use ? 0 : 1;
+      }
+    }
+    int has_mode = 0;
+    const int idle = __builtin_popcountll(sum.idle_mask);
+    for (size_t p = 0; p < n.gpus.size(); ++p) {
+      const GpuDevice& g = n.gpus[p];
+      has_mode += g.partition.compute == mode;
+      if (g.partition.compute == mode && g.healthy() && !g.partition.switching &&
+          (!memory || g.partition.memory == *memory))
+        have += sum.free_slices[p];
+    }
+    if (idle == 0) continue;
+    for (size_t p = 0; p < n.gpus.size() && p < 64; ++p) {
+      const GpuDevice& g = n.gpus[p];
+      const bool wrong = g.partition.compute != mode || (memory && g.partition.memory != *memory);
+      if (wrong && (sum.idle_mask >> p & 1)) cands.push_back({&kv.first, &g, has_mode, idle, cands.size()});
+    }
+  }
   if (have >= count) return out;
   const int per_gpu = partition_count(mode);
   // Candidate idle GPUs in a different mode; prefer nodes already running the
   // target mode (consolidation), then nodes with the fewest idle GPUs (keep
   // whole idle nodes intact for large training jobs), then SPX sources.
-  struct Cand {
-    std::string node;
-    const GpuDevice* g;
-    int node_has_mode, node_idle;
-  };
-  std::vector<Cand> cands;
-  for (const auto& kv : snap->nodes) {
-    if (within && !within->count(kv.first)) continue;
-    int has_mode = 0, idle = 0;
-    for (const auto& g : kv.second.gpus) {
-      has_mode += g.partition.compute == mode;
-      idle += gpu_idle(g);
-    }
-    for (const auto& g : kv.second.gpus) {
-      const bool wrong = g.partition.compute != mode || (memory && g.partition.memory != *memory);
-      if (wrong && gpu_idle(g)) cands.push_back({kv.first, &g, has_mode, idle});
-    }
-  }
-  std::stable_sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+  auto better = [](const Cand& a, const Cand& b) {
     if (a.node_has_mode != b.node_has_mode) return a.node_has_mode > b.node_has_mode;
     if (a.node_idle != b.node_idle) return a.node_idle < b.node_idle;
     const bool as = a.g->partition.compute == ComputePartition::SPX;
     const bool bs = b.g->partition.compute == ComputePartition::SPX;
     if (as != bs) return as;
-    return a.g->index < b.g->index;
-  });
-  for (const auto& c : cands) {
-    if (have >= count) break;
-    PartitionOp op = execute(c.node, *c.g, mode,
+    if (a.g->index != b.g->index) return a.g->index < b.g->index;
+    return a.seq < b.seq;
+  };
+  // Only the few best candidates are needed (usually one GPU): order those,
+  // and the rest only if conversions keep failing.
+  size_t sorted = 0, next = 0;
+  while (have < count && next < cands.size()) {
+    if (next >= sorted) {
+      const size_t want = static_cast<size_t>((count - have + per_gpu - 1) / per_gpu) + 4;
+      const size_t upto = std::min(cands.size(), sorted + want);
+      std::partial_sort(cands.begin() + sorted, cands.begin() + upto, cands.end(), better);
+      sorted = upto;
+    }
+    const Cand& c = cands[next++];
+    PartitionOp op = execute(*c.node, *c.g, mode,
                              "capacity: need " + std::to_string(count) + " " + to_string(mode) +
                                  (memory ? std::string("/") + to_string(*memory) : std::string()) +
                                  " slices, have " + std::to_string(have),

@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <set>
 
 namespace kgwe {
@@ -217,7 +219,35 @@ size_t Platform::queue_depth() const {
   return pending_.size();
 }
 
+namespace {
+// Slow-verb log: with KGWE_SLOW_VERB_MS=<ms> set, a filter call that takes
+// longer prints where its time went (stderr), for chasing latency tails.
+struct PhaseLog {
+  double limit_ms;
+  int64_t t0, last;
+  char buf[256];
+  int n = 0;
+  PhaseLog() : limit_ms([] {
+      const char* e = std::getenv("KGWE_SLOW_VERB_MS");
+      return e ? std::atof(e) : 0.0;
+    }()), t0(limit_ms > 0 ? now_ns() : 0), last(t0) {}
+  void mark(const char* what) {
+    if (limit_ms <= 0) return;
+    const int64_t t = now_ns();
+    n += std::snprintf(buf + n, sizeof buf - static_cast<size_t>(n), " %s=%.2f", what, (t - last) / 1e6);
+    if (n > 200) n = 200;
+    last = t;
+  }
+  void done(const char* verb, size_t cands) {
+    if (limit_ms <= 0) return;
+    const double total = (now_ns() - t0) / 1e6;
+    if (total >= limit_ms) std::fprintf(stderr, "kgwe slow %s %.2f ms (%zu candidates):%s\n", verb, total, cands, buf);
+  }
+};
+}  // namespace
+
 std::string Platform::filter(const std::string& body) {
+  PhaseLog pl;
   // Fast path: zero-copy scan (names + byte spans of the Node items); the
   // reply splices the passing items' original bytes.  Fallback: full parse.
   ExtenderArgsScan scan;
@@ -247,46 +277,72 @@ std::string Platform::filter(const std::string& body) {
     }
     for (const auto& n : field(parsed, "nodenames", "NodeNames").items()) scan.nodenames.push_back(n.str());
   }
+  pl.mark("scan");
   const Json& pod = scan.pod;
   WorkloadRequest w = workload_from_pod(pod, cfg_.gpu_resource);
   // Microsecond creation stamp written by kgwe's mutating webhook (the
   // apiserver's creationTimestamp is whole seconds); else first filter call.
   remember_pod(w.uid, w,
                std::atof(pod.get("metadata").get("annotations").get("kgwe.amd.com/created-at").str("0").c_str()));
+  pl.mark("pod");
   std::vector<std::string> names;
   names.reserve(scan.nodes.size() + scan.nodenames.size());
   for (const auto& n : scan.nodes) names.push_back(n.name);
   for (const auto& n : scan.nodenames) names.push_back(n);
-  Json failed = Json::object();
-  std::vector<std::string> passed;
+  std::vector<std::string> why;  // per candidate: "" = passes, else the reason
+  // The reply is written straight into its string: failedNodes, then the
+  // passing candidates in request order (Node items are spliced from the
+  // request's own bytes).
   auto reply = [&]() {
-    std::string out = "{\"failedNodes\":";
-    failed.dump_to(out);
+    std::string out;
+    out.reserve(64 + names.size() * 48);
+    out += "{\"failedNodes\":{";
+    bool first = true;
+    for (size_t i = 0; i < names.size(); ++i)
+      if (!why[i].empty()) {
+        if (!first) out += ',';
+        first = false;
+        out += '"';
+        out += json_escape(names[i]);
+        out += "\":\"";
+        out += json_escape(why[i]);
+        out += '"';
+      }
+    out += '}';
     if (scan.have_nodes) {
-      std::set<std::string> ok(passed.begin(), passed.end());
       out += ",\"nodes\":{\"items\":[";
-      bool first = true;
+      first = true;
       if (scanned) {
-        for (const auto& n : scan.nodes)
-          if (ok.count(n.name)) {
+        for (size_t i = 0; i < scan.nodes.size(); ++i)
+          if (why[i].empty()) {
             if (!first) out += ',';
-            out.append(body, n.begin, n.end - n.begin);
+            out.append(body, scan.nodes[i].begin, scan.nodes[i].end - scan.nodes[i].begin);
             first = false;
           }
       } else {
-        for (const auto& n : field(parsed, "nodes", "Nodes").get("items").items())
-          if (ok.count(n.get("metadata").get("name").str())) {
+        size_t i = 0;
+        for (const auto& n : field(parsed, "nodes", "Nodes").get("items").items()) {
+          if (i < why.size() && why[i].empty()) {
             if (!first) out += ',';
             n.dump_to(out);
             first = false;
           }
+          ++i;
+        }
       }
       out += "]}";
     } else {
-      Json nn = Json::array();
-      for (const auto& n : passed) nn.push_back(n);
-      out += ",\"nodenames\":";
-      nn.dump_to(out);
+      out += ",\"nodenames\":[";
+      first = true;
+      for (size_t i = 0; i < names.size(); ++i)
+        if (why[i].empty()) {
+          if (!first) out += ',';
+          first = false;
+          out += '"';
+          out += json_escape(names[i]);
+          out += '"';
+        }
+      out += ']';
     }
     out += "}";
     return out;
@@ -298,27 +354,35 @@ std::string Platform::filter(const std::string& body) {
                                    : p.on_demand * w.gpu_count;
     Admission a = cost_->admit(w.ns, w.team, w.project, est, wall_s());
     if (!a.allowed) {
-      for (const auto& n : names) failed[n] = a.reason;
+      why.assign(names.size(), a.reason);
       reg_->add("kgwe_scheduling_failures_total", {"budget"}, 1);
       return reply();
     }
   }
-  auto fails = sched_->filter(w, names, &passed);
-  if (passed.empty() && w.partition && cfg_.auto_provision_partitions) {
+  pl.mark("admit");
+  auto any_passed = [&why]() {
+    for (const auto& v : why)
+      if (v.empty()) return true;
+    return false;
+  };
+  sched_->filter_verdicts(w, names, &why);
+  pl.mark("verdicts");
+  if (!any_passed() && w.partition && cfg_.auto_provision_partitions) {
     const std::unordered_set<std::string> cand(names.begin(), names.end());
     auto ops = part_->ensure_capacity(w.partition_mode, w.partition_count, false,
                                       w.partition_memory_set ? &w.partition_memory : nullptr, &cand);
     for (const auto& op : ops)
       reg_->add("kgwe_partition_reconfigurations_total",
                 {op.node, op.state == OpState::Failed ? "failed" : "ok"}, 1);
-    if (!ops.empty()) {
-      passed.clear();
-      fails = sched_->filter(w, names, &passed);
-    }
+    pl.mark("provision");
+    if (!ops.empty()) sched_->filter_verdicts(w, names, &why);
+    pl.mark("verdicts2");
   }
-  for (const auto& kv : fails) failed[kv.first] = kv.second;
-  if (passed.empty()) reg_->add("kgwe_scheduling_failures_total", {"filter"}, 1);
-  return reply();
+  if (!any_passed()) reg_->add("kgwe_scheduling_failures_total", {"filter"}, 1);
+  std::string out = reply();
+  pl.mark("reply");
+  pl.done("filter", names.size());
+  return out;
 }
 
 std::string Platform::prioritize(const std::string& body) {
@@ -349,15 +413,22 @@ std::string Platform::prioritize(const std::string& body) {
   std::vector<std::string> names;
   for (const auto& n : scan.nodes) names.push_back(n.name);
   for (const auto& n : scan.nodenames) names.push_back(n);
-  Json out = Json::array();
-  for (const auto& s : sched_->prioritize(w, names)) {
-    Json h = Json::object();
-    h["host"] = s.node;
+  std::vector<int> totals;
+  sched_->prioritize_totals(w, names, &totals);
+  std::string out;
+  out.reserve(8 + names.size() * 40);
+  out += '[';
+  for (size_t i = 0; i < names.size(); ++i) {
+    if (i) out += ',';
+    out += "{\"host\":\"";
+    out += json_escape(names[i]);
+    out += "\",\"score\":";
     // kube-scheduler MaxExtenderPriority = 10; our totals are 0..~120.
-    h["score"] = static_cast<int64_t>(std::min(10.0, std::round(s.total / 10.0)));
-    out.push_back(h);
+    out += std::to_string(static_cast<int>(std::min(10.0, std::round(totals[i] / 10.0))));
+    out += '}';
   }
-  return out.dump();
+  out += ']';
+  return out;
 }
 
 std::string Platform::preempt(const std::string& body) {
@@ -412,20 +483,30 @@ std::string Platform::placement_json(const WorkloadRequest& w, const Decision& d
 }
 
 std::string Platform::bind(const std::string& body, const std::string& pod_json) {
+  return bind_outcome(body, pod_json).json;
+}
+
+Platform::BindOutcome Platform::bind_outcome(const std::string& body, const std::string& pod_json) {
+  BindOutcome bo;
   Json out = Json::object();
   Json res = Json::object();
   Json args;
   try {
     args = Json::parse(body);
   } catch (const std::exception& e) {
-    res["error"] = std::string("bad ExtenderBindingArgs: ") + e.what();
+    bo.error = std::string("bad ExtenderBindingArgs: ") + e.what();
+    res["error"] = bo.error;
     out["result"] = res;
-    return out.dump();
+    bo.json = out.dump();
+    return bo;
   }
   const std::string name = field(args, "podName", "PodName").str();
   const std::string ns = field(args, "podNamespace", "PodNamespace").str("default");
   std::string uid = field(args, "podUID", "PodUID").str();
   const std::string node = field(args, "node", "Node").str();
+  bo.ns = ns;
+  bo.name = name;
+  bo.node = node;
   WorkloadRequest w;
   bool have = false;
   if (!pod_json.empty()) {
@@ -447,35 +528,49 @@ std::string Platform::bind(const std::string& body, const std::string& pod_json)
       have = true;
     }
   }
+  bo.uid = uid;
   if (!have) {
-    res["error"] = "unknown pod " + ns + "/" + name + " (no filter call seen)";
+    bo.unknown_pod = true;
+    bo.error = "unknown pod " + ns + "/" + name + " (no filter call seen)";
+    res["error"] = bo.error;
     out["result"] = res;
-    return out.dump();
+    bo.json = out.dump();
+    return bo;
   }
+  bo.uid = w.uid;
+  bo.gang = w.gang;
   Decision d = sched_->bind(w, node);
   if (!d.ok) {
     auto it = d.failed_nodes.find(node);
-    res["error"] = it != d.failed_nodes.end() ? it->second : "bind failed";
+    bo.error = it != d.failed_nodes.end() ? it->second : "bind failed";
+    res["error"] = bo.error;
     reg_->add("kgwe_scheduling_failures_total", {"bind"}, 1);
   } else if (d.status == "Waiting") {
-    // Gang member reserved; kube-scheduler retries bind until the gang is
-    // complete (Permit semantics) or the reservation times out.
-    res["error"] = "gang " + w.gang + " waiting for members";
+    // Gang member reserved (Permit "Wait"): a serving shell holds the request
+    // until the gang is complete or the reservation times out; a caller that
+    // cannot hold it sees this error and calls bind again.
+    bo.waiting = true;
+    bo.error = "gang " + w.gang + " waiting for members";
+    res["error"] = bo.error;
   } else {
+    bo.ok = true;
     reg_->add("kgwe_scheduling_successes_total", {}, 1);
     // Pod create -> bind latency, recorded by the extender itself at every
     // successful bind (the reference declares the histogram and never feeds
     // it: prometheus_exporter.go:643-648).
     std::pair<int64_t, double> seen{0, 0.0};
+    bool first = false;
     {
       std::lock_guard<std::mutex> lk(pods_mu_);
       auto it = pending_.find(w.uid);
       if (it != pending_.end()) {
         seen = it->second;
         pending_.erase(it);
+        first = true;
       }
     }
     double created = seen.second;
+    if (!pod_json.empty()) first = true;  // bound from the pod object (no filter call seen)
     if (created <= 0 && !pod_json.empty()) {
       try {
         created = std::atof(Json::parse(pod_json).get("metadata").get("annotations")
@@ -483,23 +578,26 @@ std::string Platform::bind(const std::string& body, const std::string& pod_json)
       } catch (...) {
       }
     }
-    if (created > 0) observe_pod_latency_ms(std::max(0.0, (wall_s() - created) * 1000.0));
-    else if (seen.first > 0) observe_pod_latency_ms(static_cast<double>(now_ns() - seen.first) / 1e6);
-    UsageRecord r;
-    r.uid = w.uid;
-    r.ns = w.ns;
-    r.team = w.team;
-    r.project = w.project;
-    r.gpu_type = "amd-mi355x-288gb";
-    r.gpu_count = w.partition ? w.partition_count : w.gpu_count;
-    r.partition_mode = w.partition ? to_string(w.partition_mode) : "";
-    cost_->start(r, wall_s());
-    if (w.partition) reg_->add("kgwe_partition_allocations_total", {to_string(w.partition_mode)}, 1);
+    if (first) {  // an idempotent re-bind of a bound pod is not a second sample
+      if (created > 0) observe_pod_latency_ms(std::max(0.0, (wall_s() - created) * 1000.0));
+      else if (seen.first > 0) observe_pod_latency_ms(static_cast<double>(now_ns() - seen.first) / 1e6);
+      UsageRecord r;
+      r.uid = w.uid;
+      r.ns = w.ns;
+      r.team = w.team;
+      r.project = w.project;
+      r.gpu_type = "amd-mi355x-288gb";
+      r.gpu_count = w.partition ? w.partition_count : w.gpu_count;
+      r.partition_mode = w.partition ? to_string(w.partition_mode) : "";
+      cost_->start(r, wall_s());
+      if (w.partition) reg_->add("kgwe_partition_allocations_total", {to_string(w.partition_mode)}, 1);
+    }
   }
   reg_->add("kgwe_scheduling_attempts_total", {}, 1);
   out["result"] = res;
   out["placement"] = Json::parse(placement_json(w, d));
-  return out.dump();
+  bo.json = out.dump();
+  return bo;
 }
 
 std::string Platform::schedule(const std::string& workload_json) {
@@ -598,6 +696,7 @@ void Platform::tick(double now_s) {
 }
 
 void Platform::refresh_gauges(double now_s) {
+  std::lock_guard<std::mutex> refresh_lk(gauges_mu_);  // tick and a scrape may both come here
   auto snap = disc_->snapshot();
   GaugeBatch batch;  // built off-lock, swapped in at the end
   for (const char* f : {"kgwe_gpu_count", "kgwe_gpu_utilization_percent", "kgwe_gpu_gfx_activity_percent",
@@ -613,67 +712,93 @@ void Platform::refresh_gauges(double now_s) {
                         "kgwe_cost_savings_recommended_dollars", "kgwe_gpu_cost_per_hour_dollars",
                         "kgwe_gpu_share_clients"})
     batch.touch(f);
+  const std::vector<Allocation> allocs = sched_->allocations();
   std::set<std::string> owned_parts;
-  for (const auto& a : sched_->allocations())
+  for (const auto& a : allocs)
     for (const auto& p : a.partitions) owned_parts.insert(p);
+  // Everything that derives from a node's topology object alone goes into
+  // per-node blocks, rebuilt only for nodes whose object changed since the
+  // last refresh: at 10,000 GPUs a from-scratch refresh is ~250,000 series
+  // (~0.5 s of CPU, and a million small allocations whose release stalled the
+  // next allocation of the same thread for ~150 ms).
+  for (auto it = node_gauges_.begin(); it != node_gauges_.end();)
+    it = snap->nodes.count(it->first) ? std::next(it) : node_gauges_.erase(it);
   for (const auto& kv : snap->nodes) {
     const NodeTopology& n = kv.second;
-    batch.set("kgwe_gpu_count", {n.name}, static_cast<double>(n.gpus.size()));
+    NodeGauges& ng = node_gauges_[n.name];
+    if (ng.topo != &n || ng.updated_ns != n.updated_ns || ng.blocks.empty()) {
+      std::map<std::string, MetricRegistry::Block> b;
+      b["kgwe_gpu_count"].push_back({{n.name}, static_cast<double>(n.gpus.size())});
+      int links_up = 0, links = 0;
+      for (const auto& g : n.gpus) {
+        b["kgwe_gpu_utilization_percent"].push_back({{g.uuid, n.name, g.model}, g.util.gfx_activity});
+        b["kgwe_gpu_gfx_activity_percent"].push_back({{g.uuid, n.name}, g.util.gfx_activity});
+        b["kgwe_gpu_umc_activity_percent"].push_back({{g.uuid, n.name}, g.util.umc_activity});
+        b["kgwe_gpu_memory_used_bytes"].push_back({{g.uuid, n.name}, g.memory_used_gb * 1073741824.0});
+        b["kgwe_gpu_memory_total_bytes"].push_back({{g.uuid, n.name}, g.memory_total_gb * 1073741824.0});
+        b["kgwe_gpu_temperature_celsius"].push_back({{g.uuid, n.name}, g.util.temperature_c});
+        b["kgwe_gpu_power_watts"].push_back({{g.uuid, n.name}, g.util.power_w});
+        b["kgwe_gpu_health_status"].push_back(
+            {{g.uuid, n.name}, g.health.status == HealthStatus::Healthy ? 1.0
+                               : g.health.status == HealthStatus::Degraded ? 0.5 : 0.0});
+        if (g.hbm_measured_gbps > 0)
+          b["kgwe_gpu_hbm_bandwidth_gbps"].push_back({{g.uuid, n.name}, g.hbm_measured_gbps});
+        auto& ecc = b["kgwe_gpu_ecc_errors_total"];
+        ecc.push_back({{g.uuid, n.name, "correctable"}, static_cast<double>(g.health.ecc_correctable)});
+        ecc.push_back({{g.uuid, n.name, "uncorrectable"}, static_cast<double>(g.health.ecc_uncorrectable)});
+        ecc.push_back({{g.uuid, n.name, "deferred"}, static_cast<double>(g.health.ecc_deferred)});
+        auto& rp = b["kgwe_gpu_retired_pages"];
+        rp.push_back({{g.uuid, n.name, "retired"}, static_cast<double>(g.health.retired_pages)});
+        rp.push_back({{g.uuid, n.name, "pending"}, static_cast<double>(g.health.pending_retired_pages)});
+        b["kgwe_gpu_xgmi_errors"].push_back({{g.uuid, n.name}, static_cast<double>(g.health.xgmi_errors)});
+        auto& cp = b["kgwe_gpu_cper_records"];
+        cp.push_back({{g.uuid, n.name, "fatal"}, static_cast<double>(g.health.cper_fatal)});
+        cp.push_back({{g.uuid, n.name, "uncorrected"}, static_cast<double>(g.health.cper_uncorrected)});
+        cp.push_back({{g.uuid, n.name, "corrected"}, static_cast<double>(g.health.cper_corrected)});
+        for (const auto& t : g.health.throttle_reasons)
+          b["kgwe_gpu_throttle_active"].push_back({{g.uuid, n.name, t}, 1.0});
+        b["kgwe_gpu_partition_mode"].push_back(
+            {{g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0});
+        b["kgwe_partition_instance_count"].push_back(
+            {{g.uuid, n.name, to_string(g.partition.compute)}, static_cast<double>(g.partition.instances.size())});
+        b["kgwe_pcie_bandwidth_gbps"].push_back({{g.uuid, n.name}, g.pcie.bandwidth_gbps});
+        for (const auto& l : g.links) {
+          b["kgwe_xgmi_bandwidth_gbps"].push_back({{g.uuid, l.peer_uuid, n.name}, l.up ? l.effective_gbps() : 0.0});
+          b["kgwe_xgmi_link_status"].push_back({{g.uuid, l.peer_uuid, n.name}, l.up ? 1.0 : 0.0});
+          ++links;
+          links_up += l.up && l.type == LinkType::XGMI;
+        }
+      }
+      // Node topology score: 50 base, +30 full xGMI mesh, +20 proportional link health.
+      const double ts = 50.0 + (n.xgmi_fully_connected ? 30.0 : 0.0) + (links ? 20.0 * links_up / links : 0.0);
+      b["kgwe_topology_score"].push_back({{n.name}, ts});
+      ng.topo = &n;
+      ng.updated_ns = n.updated_ns;
+      ng.blocks.clear();
+      for (auto& fb : b)
+        ng.blocks[fb.first] = std::make_shared<const MetricRegistry::Block>(std::move(fb.second));
+    }
+    for (const auto& fb : ng.blocks) batch.block(fb.first, n.name, fb.second);
+    // Slice occupancy depends on the ledger: computed every time, only for
+    // nodes that have partitioned GPUs.
     std::map<std::string, std::pair<int, int>> slices;  // mode -> (used, total)
-    int links_up = 0, links = 0;
     for (const auto& g : n.gpus) {
-      batch.set("kgwe_gpu_utilization_percent", {g.uuid, n.name, g.model}, g.util.gfx_activity);
-      batch.set("kgwe_gpu_gfx_activity_percent", {g.uuid, n.name}, g.util.gfx_activity);
-      batch.set("kgwe_gpu_umc_activity_percent", {g.uuid, n.name}, g.util.umc_activity);
-      batch.set("kgwe_gpu_memory_used_bytes", {g.uuid, n.name}, g.memory_used_gb * 1073741824.0);
-      batch.set("kgwe_gpu_memory_total_bytes", {g.uuid, n.name}, g.memory_total_gb * 1073741824.0);
-      batch.set("kgwe_gpu_temperature_celsius", {g.uuid, n.name}, g.util.temperature_c);
-      batch.set("kgwe_gpu_power_watts", {g.uuid, n.name}, g.util.power_w);
-      batch.set("kgwe_gpu_health_status", {g.uuid, n.name},
-                g.health.status == HealthStatus::Healthy ? 1.0
-                : g.health.status == HealthStatus::Degraded ? 0.5 : 0.0);
-      if (g.hbm_measured_gbps > 0) batch.set("kgwe_gpu_hbm_bandwidth_gbps", {g.uuid, n.name}, g.hbm_measured_gbps);
-      batch.set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "correctable"}, static_cast<double>(g.health.ecc_correctable));
-      batch.set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "uncorrectable"}, static_cast<double>(g.health.ecc_uncorrectable));
-      batch.set("kgwe_gpu_ecc_errors_total", {g.uuid, n.name, "deferred"}, static_cast<double>(g.health.ecc_deferred));
-      batch.set("kgwe_gpu_retired_pages", {g.uuid, n.name, "retired"}, static_cast<double>(g.health.retired_pages));
-      batch.set("kgwe_gpu_retired_pages", {g.uuid, n.name, "pending"},
-                static_cast<double>(g.health.pending_retired_pages));
-      batch.set("kgwe_gpu_xgmi_errors", {g.uuid, n.name}, static_cast<double>(g.health.xgmi_errors));
-      batch.set("kgwe_gpu_cper_records", {g.uuid, n.name, "fatal"}, static_cast<double>(g.health.cper_fatal));
-      batch.set("kgwe_gpu_cper_records", {g.uuid, n.name, "uncorrected"},
-                static_cast<double>(g.health.cper_uncorrected));
-      batch.set("kgwe_gpu_cper_records", {g.uuid, n.name, "corrected"}, static_cast<double>(g.health.cper_corrected));
-      for (const auto& t : g.health.throttle_reasons) batch.set("kgwe_gpu_throttle_active", {g.uuid, n.name, t}, 1.0);
-      batch.set("kgwe_gpu_partition_mode", {g.uuid, n.name, to_string(g.partition.compute), to_string(g.partition.memory)}, 1.0);
-      batch.set("kgwe_partition_instance_count", {g.uuid, n.name, to_string(g.partition.compute)},
-                static_cast<double>(g.partition.instances.size()));
+      if (g.partition.compute == ComputePartition::SPX) continue;
       auto& sl = slices[to_string(g.partition.compute)];
       for (const auto& pi : g.partition.instances) {
         sl.second++;
         sl.first += (pi.in_use || owned_parts.count(pi.id)) ? 1 : 0;
       }
-      batch.set("kgwe_pcie_bandwidth_gbps", {g.uuid, n.name}, g.pcie.bandwidth_gbps);
-      for (const auto& l : g.links) {
-        batch.set("kgwe_xgmi_bandwidth_gbps", {g.uuid, l.peer_uuid, n.name}, l.up ? l.effective_gbps() : 0.0);
-        batch.set("kgwe_xgmi_link_status", {g.uuid, l.peer_uuid, n.name}, l.up ? 1.0 : 0.0);
-        ++links;
-        links_up += l.up && l.type == LinkType::XGMI;
-      }
     }
-    for (const auto& s : slices)
-      if (s.first != "SPX")
-        batch.set("kgwe_partition_instance_utilization_percent", {n.name, s.first},
-                  s.second.second ? 100.0 * s.second.first / s.second.second : 0.0);
-    // Node topology score: 50 base, +30 full xGMI mesh, +20 proportional link health.
-    double ts = 50.0 + (n.xgmi_fully_connected ? 30.0 : 0.0) + (links ? 20.0 * links_up / links : 0.0);
-    batch.set("kgwe_topology_score", {n.name}, ts);
+    for (const auto& sl : slices)
+      batch.set("kgwe_partition_instance_utilization_percent", {n.name, sl.first},
+                sl.second.second ? 100.0 * sl.second.first / sl.second.second : 0.0);
   }
-  for (const auto& a : sched_->allocations())
+  for (const auto& a : allocs)
     if (!a.shared_gpu.empty())
       batch.add("kgwe_gpu_share_clients", {a.shared_gpu, a.node, to_string(a.sharing)}, 1.0);
   std::map<std::pair<std::string, std::string>, int> active;
-  for (const auto& a : sched_->allocations()) active[{a.ns, to_string(a.type)}]++;
+  for (const auto& a : allocs) active[{a.ns, to_string(a.type)}]++;
   for (const auto& kv : active)
     batch.set("kgwe_active_workloads", {kv.first.first, kv.first.second}, kv.second);
   for (const auto& b : cost_->budgets(now_s))

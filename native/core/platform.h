@@ -73,6 +73,18 @@ class Platform {
   std::string preempt(const std::string& body);
   // Returns {"result": ExtenderBindingResult, "placement": {...}}.
   std::string bind(const std::string& body, const std::string& pod_json = "");
+  // bind() plus what a serving shell needs to act on the result without
+  // re-parsing it.  `waiting`: the pod is a gang member whose GPUs are
+  // reserved but whose gang is not complete yet (the scheduler framework's
+  // Permit "Wait"); calling bind again once the gang is ready returns ok.
+  struct BindOutcome {
+    std::string json;   // what bind() returns
+    bool ok = false;    // bound: placement is final
+    bool waiting = false;
+    bool unknown_pod = false;  // no filter call seen for this pod (and no pod_json)
+    std::string uid, ns, name, node, gang, error;
+  };
+  BindOutcome bind_outcome(const std::string& body, const std::string& pod_json = "");
 
   // Direct API (controller / optimizer / tests).
   std::string schedule(const std::string& workload_json);
@@ -117,6 +129,15 @@ class Platform {
   // tick() refreshes gauges at most at a 10 % duty cycle: at 10,000 GPUs a
   // refresh is ~0.5 s of CPU, and a scrape refreshes them anyway.
   std::atomic<int64_t> gauges_next_ns_{0};
+  // Per-node gauge blocks of the last refresh, re-used while the node's
+  // topology object is the same one (nothing about it changed).
+  struct NodeGauges {
+    const NodeTopology* topo = nullptr;
+    int64_t updated_ns = 0;
+    std::map<std::string, std::shared_ptr<const MetricRegistry::Block>> blocks;
+  };
+  std::mutex gauges_mu_;
+  std::map<std::string, NodeGauges> node_gauges_;
 };
 
 }  // namespace kgwe

@@ -1,6 +1,8 @@
 #include "scheduler.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <functional>
 #include <numeric>
@@ -432,6 +434,7 @@ Scheduler::Scheduler(std::shared_ptr<DiscoveryService> disc, SchedulerConfig cfg
 void Scheduler::set_config(const SchedulerConfig& c) {
   std::unique_lock<RwLock> lk(mu_);
   cfg_ = c;
+  global_gen_.fetch_add(1);
 }
 
 // Caller holds mu_ (shared or unique).
@@ -474,6 +477,7 @@ void Scheduler::set_cordon(const std::string& node, bool on) {
   std::lock_guard<std::mutex> lk(cordon_mu_);
   if (on) cordoned_.insert(node);
   else cordoned_.erase(node);
+  global_gen_.fetch_add(1);
 }
 
 std::vector<std::string> Scheduler::cordoned() const {
@@ -1096,6 +1100,294 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
   return s;
 }
 
+// ---------------------------------------------------------------------------
+// Per-node verdict / score memo (see NodeCache in scheduler.h).
+// ---------------------------------------------------------------------------
+Scheduler::NodeCache& Scheduler::cache_of(const std::string& node) const {
+  {
+    std::shared_lock<std::shared_mutex> lk(cache_map_mu_);
+    auto it = node_cache_.find(node);
+    if (it != node_cache_.end()) return *it->second;
+  }
+  std::unique_lock<std::shared_mutex> lk(cache_map_mu_);
+  auto& p = node_cache_[node];
+  if (!p) p = std::make_unique<NodeCache>();
+  return *p;
+}
+
+void Scheduler::touch_node(const std::string& node) {
+  cache_of(node).epoch.fetch_add(1, std::memory_order_release);
+}
+
+uint64_t Scheduler::request_signature(const WorkloadRequest& w) {
+  if (!w.anti_affinity_with.empty() || !w.colocate_with.empty()) return 0;
+  uint64_t h = 1469598103934665603ull;
+  auto bytes = [&h](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  auto num = [&](double v) { bytes(&v, sizeof v); };
+  auto str = [&](const std::string& s) {
+    bytes(s.data(), s.size());
+    const unsigned char sep = 0xff;
+    bytes(&sep, 1);
+  };
+  num(w.gpu_count);
+  num(w.min_memory_gb);
+  num(w.min_bandwidth_gbps);
+  num(static_cast<int>(w.topology));
+  str(w.arch);
+  str(w.model);
+  num(w.partition);
+  num(static_cast<int>(w.partition_mode));
+  num(w.partition_count);
+  num(w.partition_memory_set);
+  num(static_cast<int>(w.partition_memory));
+  num(static_cast<int>(w.strategy));
+  num(static_cast<int>(w.sharing));
+  num(w.share_cu_percent);
+  num(w.share_memory_gb);
+  for (const auto& kv : w.node_selector) {
+    str(kv.first);
+    str(kv.second);
+  }
+  for (const auto* terms : {&w.required_affinity, &w.preferred_affinity}) {
+    num(static_cast<double>(terms->size()));
+    for (const auto& t : *terms) {
+      str(t.key);
+      str(t.op);
+      num(t.weight);
+      for (const auto& v : t.values) str(v);
+    }
+  }
+  for (const auto& t : w.tolerations) {
+    str(t.key);
+    str(t.op);
+    str(t.value);
+    str(t.effect);
+  }
+  num(static_cast<double>(w.exclude_nodes.size()));
+  for (const auto& n : w.exclude_nodes) str(n);
+  num(static_cast<double>(w.preferred_nodes.size()));
+  for (const auto& n : w.preferred_nodes) str(n);
+  return (h && h != ~0ull) ? h : 1;
+}
+
+// Caller holds mu_ (shared or unique).  Returns the verdict ("" = eligible);
+// the reference stays valid until the next call with the same scratch.
+const std::string& Scheduler::eligible_cached(const NodeTopology& n, const WorkloadRequest& w, uint64_t sig,
+                                              std::string* scratch) const {
+  if (sig == 0) {
+    *scratch = eligible(n, w);
+    return *scratch;
+  }
+  NodeCache& c = cache_of(n.name);
+  const uint64_t epoch = c.epoch.load(std::memory_order_acquire);
+  const uint64_t gen = global_gen_.load(std::memory_order_acquire);
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto& e : c.entries)
+      if (e.sig == sig && e.epoch == epoch && e.gen == gen && e.topo == &n && e.topo_ns == n.updated_ns &&
+          e.has_why) {
+        e.used = ++c.clock;
+        *scratch = e.why;
+        return *scratch;
+      }
+  }
+  *scratch = eligible(n, w);
+  std::lock_guard<std::mutex> lk(c.mu);
+  NodeCacheEntry* slot = nullptr;
+  for (auto& e : c.entries)
+    if (e.sig == sig) slot = &e;
+  if (!slot) {
+    if (c.entries.size() < 12) {
+      c.entries.emplace_back();
+      slot = &c.entries.back();
+    } else {
+      slot = &*std::min_element(c.entries.begin(), c.entries.end(),
+                                [](const NodeCacheEntry& a, const NodeCacheEntry& b) { return a.used < b.used; });
+    }
+    *slot = NodeCacheEntry();
+  }
+  if (slot->epoch != epoch || slot->gen != gen || slot->topo != &n || slot->topo_ns != n.updated_ns)
+    slot->has_total = false;
+  slot->sig = sig;
+  slot->epoch = epoch;
+  slot->gen = gen;
+  slot->topo = &n;
+  slot->topo_ns = n.updated_ns;
+  slot->has_why = true;
+  slot->why = *scratch;
+  slot->used = ++c.clock;
+  return *scratch;
+}
+
+// Caller holds mu_.  Total score of an ELIGIBLE node (0 when nothing fits).
+int Scheduler::total_cached(const NodeTopology& n, const WorkloadRequest& w, uint64_t sig) const {
+  if (sig == 0) return score_node(n, w).total;
+  NodeCache& c = cache_of(n.name);
+  const uint64_t epoch = c.epoch.load(std::memory_order_acquire);
+  const uint64_t gen = global_gen_.load(std::memory_order_acquire);
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (auto& e : c.entries)
+      if (e.sig == sig && e.epoch == epoch && e.gen == gen && e.topo == &n && e.topo_ns == n.updated_ns &&
+          e.has_total) {
+        e.used = ++c.clock;
+        return e.total;
+      }
+  }
+  const int total = score_node(n, w).total;
+  std::lock_guard<std::mutex> lk(c.mu);
+  NodeCacheEntry* slot = nullptr;
+  for (auto& e : c.entries)
+    if (e.sig == sig) slot = &e;
+  if (!slot) {
+    if (c.entries.size() < 12) {
+      c.entries.emplace_back();
+      slot = &c.entries.back();
+    } else {
+      slot = &*std::min_element(c.entries.begin(), c.entries.end(),
+                                [](const NodeCacheEntry& a, const NodeCacheEntry& b) { return a.used < b.used; });
+    }
+    *slot = NodeCacheEntry();
+  }
+  if (slot->epoch != epoch || slot->gen != gen || slot->topo != &n || slot->topo_ns != n.updated_ns)
+    slot->has_why = false;
+  slot->sig = sig;
+  slot->epoch = epoch;
+  slot->gen = gen;
+  slot->topo = &n;
+  slot->topo_ns = n.updated_ns;
+  slot->has_total = true;
+  slot->total = total;
+  slot->used = ++c.clock;
+  return total;
+}
+
+Scheduler::NodeSummary Scheduler::node_summary(const NodeTopology& n) const {
+  constexpr uint64_t kSig = ~0ull;  // reserved signature of the summary entry
+  NodeCache& c = cache_of(n.name);
+  std::shared_lock<RwLock> lk(mu_);
+  const uint64_t epoch = c.epoch.load(std::memory_order_acquire);
+  const uint64_t gen = global_gen_.load(std::memory_order_acquire);
+  {
+    std::lock_guard<std::mutex> ck(c.mu);
+    for (auto& e : c.entries)
+      if (e.sig == kSig && e.epoch == epoch && e.gen == gen && e.topo == &n && e.topo_ns == n.updated_ns &&
+          e.has_summary) {
+        e.used = ++c.clock;
+        return e.summary;
+      }
+  }
+  NodeSummary out;
+  out.free_slices.assign(n.gpus.size(), 0);
+  for (size_t p = 0; p < n.gpus.size(); ++p) {
+    const GpuDevice& g = n.gpus[p];
+    if (!g.healthy() || g.partition.switching) continue;
+    const bool whole = gpu_owner_.count(g.uuid) || shared_.count(g.uuid) || fenced_.count(g.uuid);
+    bool any_busy = whole;
+    int free_n = 0;
+    for (const auto& pi : g.partition.instances) {
+      const bool taken = pi.in_use || (!part_owner_.empty() && part_owner_.count(pi.id));
+      any_busy |= taken;
+      free_n += taken ? 0 : 1;
+    }
+    out.free_slices[p] = whole ? 0 : static_cast<uint8_t>(std::min(free_n, 255));
+    if (!any_busy && g.util.gfx_activity < 5.0 && p < 64) out.idle_mask |= 1ull << p;
+  }
+  std::lock_guard<std::mutex> ck(c.mu);
+  NodeCacheEntry* slot = nullptr;
+  for (auto& e : c.entries)
+    if (e.sig == kSig) slot = &e;
+  if (!slot) {
+    if (c.entries.size() < 12) {
+      c.entries.emplace_back();
+      slot = &c.entries.back();
+    } else {
+      slot = &*std::min_element(c.entries.begin(), c.entries.end(),
+                                [](const NodeCacheEntry& a, const NodeCacheEntry& b) { return a.used < b.used; });
+    }
+  }
+  *slot = NodeCacheEntry();
+  slot->sig = kSig;
+  slot->epoch = epoch;
+  slot->gen = gen;
+  slot->topo = &n;
+  slot->topo_ns = n.updated_ns;
+  slot->has_summary = true;
+  slot->summary = out;
+  slot->used = ++c.clock;
+  return out;
+}
+
+void Scheduler::filter_verdicts(const WorkloadRequest& w, const std::vector<std::string>& nodes,
+                                std::vector<std::string>* why) {
+  why->assign(nodes.size(), std::string());
+  auto snap = disc_->snapshot();
+  const uint64_t sig = request_signature(w);
+  std::string scratch;
+  // The ledger is read in chunks of kSweepChunk nodes: a sweep over 1,250
+  // candidates must not hold binds / releases off the ledger for its whole
+  // length (each node's verdict is advisory anyway: bind re-checks).
+  static const bool dbg = std::getenv("KGWE_SLOW_VERB_MS") != nullptr;
+  int64_t wait_ns = 0, t_l = dbg ? now_ns() : 0, worst_node_ns = 0;
+  std::shared_lock<RwLock> lk(mu_);
+  if (dbg) wait_ns += now_ns() - t_l;
+  auto mine = allocs_.find(w.uid);
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    if ((i + 1) % kSweepChunk == 0) {
+      lk.unlock();
+      if (dbg) t_l = now_ns();
+      lk.lock();
+      if (dbg) wait_ns += now_ns() - t_l;
+      mine = allocs_.find(w.uid);
+    }
+    const int64_t t_n = dbg ? now_ns() : 0;
+    struct NodeTimer {
+      int64_t t0, *worst;
+      bool on;
+      ~NodeTimer() {
+        if (on) *worst = std::max(*worst, now_ns() - t0);
+      }
+    } nt{t_n, &worst_node_ns, dbg};
+    if (dbg && i + 1 == nodes.size() && wait_ns + worst_node_ns > 5000000)
+      std::fprintf(stderr, "kgwe filter_verdicts: lock wait %.2f ms, worst node %.2f ms\n", wait_ns / 1e6,
+                   worst_node_ns / 1e6);
+    const std::string& name = nodes[i];
+    auto it = snap->nodes.find(name);
+    if (it == snap->nodes.end()) {
+      (*why)[i] = "node not managed by kgwe (no MI355X topology)";
+      continue;
+    }
+    if (mine != allocs_.end()) {  // already reserved (gang member / retry): only that node
+      if (mine->second.node != name) (*why)[i] = "workload already reserved on " + mine->second.node;
+      continue;
+    }
+    const std::string& v = eligible_cached(it->second, w, sig, &scratch);
+    if (!v.empty()) (*why)[i] = v;
+  }
+}
+
+void Scheduler::prioritize_totals(const WorkloadRequest& w, const std::vector<std::string>& nodes,
+                                  std::vector<int>* totals) {
+  totals->assign(nodes.size(), 0);
+  auto snap = disc_->snapshot();
+  const uint64_t sig = request_signature(w);
+  std::string scratch;
+  std::shared_lock<RwLock> lk(mu_);
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    if ((i + 1) % kSweepChunk == 0) {  // see filter_verdicts()
+      lk.unlock();
+      lk.lock();
+    }
+    auto it = snap->nodes.find(nodes[i]);
+    if (it == snap->nodes.end()) continue;
+    if (!eligible_cached(it->second, w, sig, &scratch).empty()) continue;
+    (*totals)[i] = total_cached(it->second, w, sig);
+  }
+}
+
 bool Scheduler::gpu_has_slice_owner_locked(const std::string& gpu_uuid) const {
   if (part_owner_.empty()) return false;
   for (int i = 0; i < 8; ++i)  // slice ids are "<uuid>/p<i>", at most 8 (CPX)
@@ -1103,18 +1395,22 @@ bool Scheduler::gpu_has_slice_owner_locked(const std::string& gpu_uuid) const {
   return false;
 }
 
-bool Scheduler::fence_gpu(const std::string& gpu_uuid) {
+bool Scheduler::fence_gpu(const std::string& gpu_uuid, const std::string& node) {
   std::unique_lock<RwLock> lk(mu_);
   if (gpu_owner_.count(gpu_uuid) || gpu_has_slice_owner_locked(gpu_uuid) || fenced_.count(gpu_uuid) ||
       shared_.count(gpu_uuid))
     return false;
   fenced_.insert(gpu_uuid);
+  if (node.empty()) global_gen_.fetch_add(1);
+  else touch_node(node);
   return true;
 }
 
-void Scheduler::unfence_gpu(const std::string& gpu_uuid) {
+void Scheduler::unfence_gpu(const std::string& gpu_uuid, const std::string& node) {
   std::unique_lock<RwLock> lk(mu_);
   fenced_.erase(gpu_uuid);
+  if (node.empty()) global_gen_.fetch_add(1);
+  else touch_node(node);
 }
 
 // Caller holds mu_ exclusively.  The score may come from an older topology
@@ -1139,9 +1435,8 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
     const GpuDevice* g = nit == snap->nodes.end() ? nullptr : nit->second.gpu(s.shared_gpu);
     int b = 0, e = 0;
     if (!g || !share_fits(*g, w, &b, &e)) return false;
-    if (b != s.cu_begin || e != s.cu_end) {
-      // the gap moved: take the range that fits now
-    }
+    // (b, e) may differ from the scored range when the gap moved: take the
+    // range that fits now.
     Allocation a;
     a.uid = w.uid;
     a.node = s.node;
@@ -1160,6 +1455,7 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
     sg.method = w.sharing;
     sg.clients.push_back(w.uid);
     allocs_[w.uid] = std::move(a);
+    touch_node(s.node);
     return true;
   }
   if (s.gpus.empty() && s.partitions.empty()) return false;
@@ -1182,12 +1478,14 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
   for (const auto& p : s.partitions) part_owner_[p] = w.uid;
   node_gpus_used_[s.node] += static_cast<int>(s.gpus.size());
   allocs_[w.uid] = std::move(a);
+  touch_node(s.node);
   return true;
 }
 
 // Caller holds mu_ exclusively: drop one ledger entry and everything it holds.
 void Scheduler::erase_locked(std::unordered_map<std::string, Allocation>::iterator it) {
   const Allocation& a = it->second;
+  touch_node(a.node);
   for (const auto& g : a.gpus) gpu_owner_.erase(g);
   for (const auto& p : a.partitions) part_owner_.erase(p);
   node_gpus_used_[a.node] -= static_cast<int>(a.gpus.size());
@@ -1621,32 +1919,11 @@ std::map<std::string, std::string> Scheduler::filter(const WorkloadRequest& w,
                                                      const std::vector<std::string>& nodes,
                                                      std::vector<std::string>* passed) {
   std::map<std::string, std::string> failed;
-  auto snap = disc_->snapshot();
-  // The ledger is read in chunks of kSweepChunk nodes: a sweep over 1,250
-  // candidates must not hold binds / releases off the ledger for its whole
-  // length (each node's verdict is advisory anyway: bind re-checks).
-  std::shared_lock<RwLock> lk(mu_);
-  auto mine = allocs_.find(w.uid);
-  size_t k = 0;
-  for (const auto& name : nodes) {
-    if (++k % kSweepChunk == 0) {
-      lk.unlock();
-      lk.lock();
-      mine = allocs_.find(w.uid);
-    }
-    auto it = snap->nodes.find(name);
-    if (it == snap->nodes.end()) {
-      failed[name] = "node not managed by kgwe (no MI355X topology)";
-      continue;
-    }
-    if (mine != allocs_.end()) {  // already reserved (gang member / retry): only that node
-      if (mine->second.node == name) passed->push_back(name);
-      else failed[name] = "workload already reserved on " + mine->second.node;
-      continue;
-    }
-    std::string why = eligible(it->second, w);
-    if (why.empty()) passed->push_back(name);
-    else failed[name] = why;
+  std::vector<std::string> why;
+  filter_verdicts(w, nodes, &why);
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    if (why[i].empty()) passed->push_back(nodes[i]);
+    else failed[nodes[i]] = std::move(why[i]);
   }
   return failed;
 }
@@ -1827,6 +2104,7 @@ bool Scheduler::restore(const Allocation& a) {
     c.gang_pending = false;
   }
   allocs_[a.uid] = c;
+  touch_node(a.node);
   return true;
 }
 
@@ -1851,6 +2129,8 @@ bool Scheduler::migrate_partition(const std::string& uid, const std::string& fro
     part_owner_.erase(from);
     part_owner_[to] = uid;
     *pos = to;
+    touch_node(it->second.node);
+    touch_node(to_node);
     it->second.node = to_node;
     node = to_node;
   }

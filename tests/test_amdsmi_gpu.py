@@ -42,7 +42,8 @@ def test_amdsmi_discovery_and_health_signals():
 @pytest.mark.gpu
 def test_gfx_activity_sampler_sees_load():
     """amd-smi gfx_activity is a smoothed busy %: it ramps over a few hundred
-    ms, so the check is on the loaded tail of a ~1.5 s GEMM loop."""
+    ms (over a second on some hosts), so the check is on the loaded last
+    third of a ~3 s GEMM loop."""
     import time
 
     from kgwe.utils.amdsmi_util import UtilSampler, available
@@ -52,7 +53,7 @@ def test_gfx_activity_sampler_sees_load():
     (a @ a).sum().item()  # library init / first-kernel costs outside the window
     s = UtilSampler(0, interval_s=0.02).start()
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 1.5:
+    while time.perf_counter() - t0 < 3.0:
         for _ in range(20):
             a = a @ a
             a = a / a.abs().amax().clamp_min(1e-3)
@@ -60,5 +61,5 @@ def test_gfx_activity_sampler_sees_load():
     s.stop()
     vals = [v for _, v in s.samples]
     assert len(vals) >= 20
-    tail = vals[len(vals) // 2:]
+    tail = vals[2 * len(vals) // 3:]
     assert max(vals) > 80.0 and sum(tail) / len(tail) > 60.0, vals

@@ -78,11 +78,14 @@ def test_bench_rank_refuses_mismatched_world():
 
 @pytest.mark.gpu
 def test_bench_gpus1_through_launcher_on_gpu():
-    r, lines = _run(1, ["--model", "llama3-8b", "--seq-len", "2048", "--micro-batch", "1"],
-                    timeout=400)
+    # amd-smi's gfx_activity is a smoothed busy % (it needs up to ~1 s of load
+    # to rise on some hosts): time enough steps for it to settle.
+    r, lines = _run(1, ["--model", "llama3-8b", "--seq-len", "2048", "--micro-batch", "1",
+                        "--steps", "24", "--warmup", "4"], timeout=400)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(lines[-1])
     assert out["n_gpus"] == 1 and "torch.distributed.run" in out["launcher"]
     assert out["attention"] == "kgwe_flash_attn"
+    assert out["steps"] == 24
     assert out["value"] is not None and out["value"] > 50.0
     assert out["util_whole_process_pct"] is not None

@@ -134,7 +134,7 @@ def test_restart_rebuilds_ledger(cluster):
         plat2.add_fake_node(make_fixture(f"mi355x-{i}", 8, 2))
     assert rec2.rebuild_ledger() == 1
     assert plat2.scheduler_metrics()["allocated_gpus"] == 4
-    ext2.httpd.server_close()
+    ext2.stop()
 
 
 def test_agent_push_endpoint(cluster):
@@ -142,7 +142,7 @@ def test_agent_push_endpoint(cluster):
     api, kube, plat, ext, rec = cluster
     from kgwe.core import make_fixture
     node = make_fixture("pushed", 8, 2)
-    h, p = ext.httpd.server_address[:2]
+    h, p = ext.address
     c = http.client.HTTPConnection(h, p)
     c.request("POST", "/v1/nodes/pushed/topology", body=json.dumps(node))
     assert c.getresponse().status == 200
@@ -155,7 +155,7 @@ def test_agent_push_labels_node(cluster):
     import http.client
     api, kube, plat, ext, rec = cluster
     node = plat.node("mi355x-0")
-    h, p = ext.httpd.server_address[:2]
+    h, p = ext.address
 
     def push(n):
         c = http.client.HTTPConnection(h, p)
@@ -478,6 +478,6 @@ def test_failover_keeps_scheduling_semantics_and_cost(tmp_path):
         rel = plat2.release(a["uid"])
         dur = rel["cost"]["duration_s"]
         assert dur >= time.time() - t_bind - 0.5  # metered from the first leader's bind
-        ext2.httpd.server_close()
+        ext2.stop()
     finally:
         stop()
