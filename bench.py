@@ -72,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--sched-pods", type=int, default=1500,
                     help="workloads pushed through the extender for the latency p99")
     ap.add_argument("--sched-rate", type=float, default=75.0, help="pod arrivals per second")
+    ap.add_argument("--sched-nodes", type=int, default=1250,
+                    help="fleet of the scheduling-latency row (8 MI355X each; 1250 = 10,000 GPUs)")
     ap.add_argument("--no-sched", action="store_true")
     ap.add_argument("--no-cluster", action="store_true",
                     help="skip the stock-kube vs kgwe cluster simulation row")
@@ -177,16 +179,44 @@ def start_scheduling_bench(args, world: int):
     """Child process tree (apiserver / scheduler sim / extender), CPU only."""
     import subprocess
 
+    # The reference's scale target: 10,000+ GPUs (docs/PRD.md:449) = 1,250
+    # 8-GPU nodes, node names only on the wire (nodeCacheCapable: true, the
+    # chart's default); the same load on a 64-node fleet is reported beside it.
     cmd = [sys.executable, "-m", "kgwe.bench.sched_latency", "--json", "--pods",
-           str(args.sched_pods), "--rate", str(args.sched_rate), "--job-gpus", str(max(1, world))]
-    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=HERE)
+           str(args.sched_pods), "--rate", str(args.sched_rate), "--job-gpus", str(max(1, world)),
+           "--nodes", str(args.sched_nodes), "--node-cache", "--then-nodes", "64"]
+    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=HERE,
+                            preexec_fn=_side_bench_affinity(world))
+
+
+def _side_bench_affinity(world: int, count: int = 8, skip: int = 0):
+    """preexec_fn pinning a CPU-side benchmark's process tree to `count` of the
+    LAST cores this process may use (after skipping `skip` of them), when there
+    are enough cores to leave the training ranks (Python launch threads, RCCL
+    proxies) cores of their own: the side benchmarks must not skew an 8-rank
+    step time, nor the ranks (or each other) their latency tails."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    if len(allowed) < 10 + 4 * max(1, world):
+        return None
+    cores = set(allowed[len(allowed) - skip - count:len(allowed) - skip])
+
+    def pin():
+        try:
+            os.sched_setaffinity(0, cores)
+        except OSError:
+            pass
+    return pin
 
 
 def start_cluster_sim():
     import subprocess
 
     cmd = [sys.executable, "-m", "kgwe.bench.cluster", "--json"]
-    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=HERE)
+    return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=HERE,
+                            preexec_fn=_side_bench_affinity(int(os.environ.get("WORLD_SIZE", "1")), count=2, skip=8))
 
 
 def collect(proc, what: str, timeout: float = 400.0) -> dict | None:

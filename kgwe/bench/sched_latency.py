@@ -405,11 +405,18 @@ def main(argv=None) -> int:
     ap.add_argument("--full-nodes", action="store_true")
     ap.add_argument("--node-cache", action="store_true", help="nodeCacheCapable=true (names only)")
     ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--then-nodes", type=int, default=0,
+                    help="afterwards run the same load on a fleet of this many nodes "
+                         "(reported under 'fleet_<n>_nodes')")
     ap.add_argument("--json", action="store_true")
     a = ap.parse_args(argv)
     lo, hi = (float(x) for x in a.lifetime.split(","))
     res = run(n_pods=a.pods, job_gpus=a.job_gpus, n_nodes=a.nodes, rate=a.rate, lifetime_s=(lo, hi),
               full_nodes=a.full_nodes, node_cache=a.node_cache, timeout_s=a.timeout)
+    if a.then_nodes:
+        res[f"fleet_{a.then_nodes}_nodes"] = run(
+            n_pods=a.pods, job_gpus=a.job_gpus, n_nodes=a.then_nodes, rate=a.rate, lifetime_s=(lo, hi),
+            full_nodes=a.full_nodes, node_cache=a.node_cache, timeout_s=a.timeout)
     print(json.dumps(res) if a.json else json.dumps(res, indent=1), flush=True)
     os._exit(0)  # reaper timers / daemon threads: do not wait for them
 

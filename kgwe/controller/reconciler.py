@@ -265,6 +265,13 @@ class Reconciler:
         ann = md.get("annotations") or {}
         if typ == "DELETED" or phase in ("Succeeded", "Failed"):
             rel = self.p.release(uid)
+            # a preempted gang member: the gang goes as a unit (the extender's
+            # preempt verb can only name the victims on the preemptor's node)
+            peers = set(rel.get("evict_gang_peers") or [])
+            if peers:
+                for a in self.p.allocations():
+                    if a["uid"] in peers:
+                        self.evict(a, f"gang member {uid} preempted")
             run = self._running.pop(uid, None)
             if run and self.optimizer is not None and uid not in self._evicting:
                 try:  # a finished run -> a training row of the online model

@@ -8,15 +8,19 @@ sends full Node objects in every ExtenderArgs, True sends node names only.
 When no node passes and the pod has a priority, it runs kube-scheduler's
 PostFilter with the extender's ``preempt`` verb: the extender names the
 victims per node, the stand-in evicts the cheapest node's victims (deletes
-the pods) and retries the preemptor.  Used by tests and by the latency
-benchmark where no real kube-scheduler exists.  Node objects are serialised
+the pods) and retries the preemptor.  Unschedulable pods and failed binds
+go back to the queue with kube-scheduler's pod backoff (podInitialBackoffSeconds
+1 s, doubling to podMaxBackoffSeconds 10 s), and every bind runs in its own
+thread as kube-scheduler runs each binding cycle in its own goroutine — a
+gang member's bind is held by the extender until its gang is complete
+(Permit), so binds must not queue behind one another.  Used by tests and by
+the latency benchmark where no real kube-scheduler exists.  Node objects are serialised
 once per node-list refresh (kube-scheduler keeps them encoded in its cache
 too), so the stand-in's own cost stays out of the measured latency.
 """
 from __future__ import annotations
 
 import gc
-import http.client
 import json
 import queue
 import threading
@@ -29,28 +33,32 @@ SCHEDULER_NAME = "kgwe-scheduler"
 
 
 class _Http:
+    """Extender client: one native keep-alive connection per calling thread
+    (kgwe.core.native.HttpClient: gather-write of the body parts, GIL released
+    for the round trip)."""
+
     def __init__(self, base: str):
         u = urllib.parse.urlparse(base)
         self.host, self.port, self.prefix = u.hostname, u.port, u.path.rstrip("/")
         self.local = threading.local()
 
+    def _client(self):
+        from ..core import native  # noqa: PLC0415
+
+        c = getattr(self.local, "c", None)
+        if c is None:
+            c = self.local.c = native.HttpClient(self.host, self.port, 35.0)
+        return c
+
     def post(self, verb: str, obj, raw: bool = False) -> object:
-        data = obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj).encode()
-        for attempt in range(2):
-            c = getattr(self.local, "c", None)
-            if c is None:
-                c = self.local.c = http.client.HTTPConnection(self.host, self.port, timeout=30)
-            try:
-                c.request("POST", f"{self.prefix}/{verb}", body=data,
-                          headers={"Content-Type": "application/json"})
-                r = c.getresponse()
-                body = r.read() or b"null"
-                return body if raw else json.loads(body)
-            except (http.client.HTTPException, OSError):
-                self.local.c = None
-                if attempt:
-                    raise
-        return None
+        parts = obj if isinstance(obj, list) else \
+            [obj if isinstance(obj, (bytes, bytearray)) else json.dumps(obj).encode()]
+        _, body = self._client().post(f"{self.prefix}/{verb}", parts)
+        return body if raw else json.loads(body or b"null")
+
+    def post_names(self, verb: str, parts: list) -> list:
+        """POST and return only the node names of the reply (filter)."""
+        return self._client().post_names(f"{self.prefix}/{verb}", parts)[1]
 
 
 def _ready(node: dict) -> bool:
@@ -60,15 +68,19 @@ def _ready(node: dict) -> bool:
 
 class SchedulerSim:
     def __init__(self, kube: KubeClient, extender_url: str, bind_workers: int = 4,
-                 on_bound=None, on_failed=None, retry_interval_s: float = 0.05,
-                 node_cache_capable: bool = False, preempt: bool = True, on_preempted=None,
-                 node_refresh_s: float = 1.0, adaptive_nodes_to_score: bool = True):
+                 on_bound=None, on_failed=None, initial_backoff_s: float = 1.0,
+                 max_backoff_s: float = 10.0, node_cache_capable: bool = False, preempt: bool = True,
+                 on_preempted=None, node_refresh_s: float = 1.0, adaptive_nodes_to_score: bool = True,
+                 max_bind_threads: int = 256):
         self.kube = kube
         self.ext = _Http(extender_url)
         self.on_bound = on_bound
         self.on_failed = on_failed
         self.on_preempted = on_preempted
-        self.retry = retry_interval_s
+        self.backoff0, self.backoff_max = initial_backoff_s, max_backoff_s
+        self.max_bind_threads = max_bind_threads
+        self._bind_idle = 0  # binder threads waiting for work
+        self._bind_lock = threading.Lock()
         self.node_cache_capable = node_cache_capable
         self.node_refresh_s = node_refresh_s  # unused: the node cache follows a watch (see _informer)
         self.adaptive = adaptive_nodes_to_score
@@ -90,8 +102,10 @@ class SchedulerSim:
         self._threads = [threading.Thread(target=self._watch, daemon=True),
                          threading.Thread(target=self._cycle, daemon=True),
                          threading.Thread(target=self._informer, daemon=True)]
-        self._threads += [threading.Thread(target=self._binder, daemon=True)
+        self._bind_min = bind_workers
+        self._threads += [threading.Thread(target=self._binder, args=(True,), daemon=True)
                           for _ in range(bind_workers)]
+        self._n_binders = bind_workers
         self._rt = {"filter": [], "prioritize": [], "cycle": []}  # client-side round trips (s)
         self.stats = {"scheduled": 0, "unschedulable": 0, "bind_errors": 0, "preemptions": 0,
                       "preempt_calls": 0}
@@ -185,23 +199,25 @@ class SchedulerSim:
         with self._nodes_lock:
             return self._nodes
 
-    def _args(self, pod_json: bytes, names: list) -> bytes:
+    def _args(self, pod_json: bytes, names: list) -> list:
+        """ExtenderArgs as a list of body parts (sent with one gather write:
+        the cached Node objects are never joined into one buffer)."""
         if self.node_cache_capable:
-            return b'{"pod":' + pod_json + b',"nodenames":' + json.dumps(names).encode() + b"}"
+            return [b'{"pod":', pod_json, b',"nodenames":', json.dumps(names).encode(), b"}"]
         with self._nodes_lock:
             nj = self._node_json
-        return (b'{"pod":' + pod_json + b',"nodes":{"items":[' +
-                b",".join(nj[n] for n in names if n in nj) + b"]}}")
-
-    def _passed(self, reply: bytes) -> list:
-        from ..core import native  # noqa: PLC0415
-
-        try:
-            return native.scan_node_names(reply)  # C++ scanner: names of the returned items
-        except Exception:  # noqa: BLE001
-            d = json.loads(reply or b"{}")
-            return [n["metadata"]["name"] for n in (d.get("nodes") or {}).get("items", [])] + \
-                list(d.get("nodenames") or [])
+        parts = [b'{"pod":', pod_json, b',"nodes":{"items":[']
+        first = True
+        for n in names:
+            j = nj.get(n)
+            if j is None:
+                continue
+            if not first:
+                parts.append(b",")
+            parts.append(j)
+            first = False
+        parts.append(b"]}}")
+        return parts
 
     def invalidate_nodes(self) -> None:
         self._refresh_nodes()
@@ -235,9 +251,11 @@ class SchedulerSim:
             pod_json = json.dumps({k: v for k, v in pod.items() if k != "_kgwe_t"}).encode()
             try:
                 t_f = time.perf_counter()
-                passed = self._passed(self.ext.post("filter", self._args(pod_json, names), raw=True))
+                passed = self.ext.post_names("filter", self._args(pod_json, names))
                 self._rt["filter"].append(time.perf_counter() - t_f)
-            except Exception:  # noqa: BLE001
+            except Exception as e:  # noqa: BLE001 - extender unreachable / bad reply: retry with backoff
+                self.stats["cycle_errors"] = self.stats.get("cycle_errors", 0) + 1
+                self.last_error = repr(e)
                 self._requeue(pod, seen)
                 continue
             if not passed:
@@ -254,7 +272,7 @@ class SchedulerSim:
             scores = {h["host"]: h["score"] for h in pr}
             best = max(passed, key=lambda nm: (scores.get(nm, 0), -hash(nm) % 1000, nm))
             pod["_kgwe_t"]["bind_q"] = time.perf_counter()
-            self._bind_q.put((pod, best, seen))
+            self._submit_bind(pod, best, seen)
             self._rt["cycle"].append(time.perf_counter() - t_cycle)
 
     def _candidates(self, names: list) -> list:
@@ -283,6 +301,15 @@ class SchedulerSim:
             return
         plans = {n: [p["uid"] for p in (v or {}).get("pods") or []]
                  for n, v in (res.get("nodeNameToMetaVictims") or {}).items()}
+        # kube-scheduler resolves every MetaPod against the node's own pods and
+        # drops the whole extender result if one is not there
+        # (convertPodUIDToPod): a victim on another node fails the preemption.
+        for n, v in plans.items():
+            for uid in v:
+                on = self._bound.get(uid)
+                if on is not None and on[2] != n:
+                    self.stats["preempt_rejected"] = self.stats.get("preempt_rejected", 0) + 1
+                    return
         plans = {n: v for n, v in plans.items() if v}
         if not plans:
             return
@@ -302,9 +329,10 @@ class SchedulerSim:
     def _requeue(self, pod, seen):
         uid = pod["metadata"].get("uid", "")
         self.retried.add(uid)
-        # kube-scheduler backoff: doubling from the retry interval, capped at 1 s
+        # kube-scheduler's pod backoff: podInitialBackoffSeconds doubling per
+        # attempt up to podMaxBackoffSeconds (defaults 1 s and 10 s)
         n = self._attempts[uid] = self._attempts.get(uid, 0) + 1
-        delay = min(1.0, self.retry * (2 ** min(n - 1, 6)))
+        delay = min(self.backoff_max, self.backoff0 * (2 ** min(n - 1, 10)))
 
         def later():
             time.sleep(delay)
@@ -312,12 +340,32 @@ class SchedulerSim:
                 self._q.put((pod, seen))
         threading.Thread(target=later, daemon=True).start()
 
-    def _binder(self):
+    def _submit_bind(self, pod, node, seen):
+        """One binding cycle per pod, concurrently (kube-scheduler: a goroutine
+        each): a new binder thread is started whenever none is idle."""
+        with self._bind_lock:
+            spawn = self._bind_idle == 0 and self._n_binders < self.max_bind_threads
+            if spawn:
+                self._n_binders += 1
+        self._bind_q.put((pod, node, seen))
+        if spawn:
+            threading.Thread(target=self._binder, args=(False,), daemon=True).start()
+
+    def _binder(self, permanent: bool = True):
         while not self._stop.is_set():
+            with self._bind_lock:
+                self._bind_idle += 1
             try:
-                pod, node, seen = self._bind_q.get(timeout=0.2)
+                pod, node, seen = self._bind_q.get(timeout=0.2 if permanent else 2.0)
             except queue.Empty:
+                with self._bind_lock:
+                    self._bind_idle -= 1
+                    if not permanent:
+                        self._n_binders -= 1
+                        return
                 continue
+            with self._bind_lock:
+                self._bind_idle -= 1
             md = pod["metadata"]
             pod.setdefault("_kgwe_t", {})["bind"] = time.perf_counter()
             try:
@@ -326,20 +374,12 @@ class SchedulerSim:
             except Exception as e:  # noqa: BLE001
                 res = {"error": str(e)}
             if res.get("error"):
+                # a failed binding cycle (held gang bind timed out included):
+                # the pod goes back to the scheduling queue with backoff
                 self.stats["bind_errors"] += 1
-                if "waiting" in res["error"]:
-                    self._requeue_bind(pod, node, seen)
-                else:
-                    self._requeue(pod, seen)
+                self._requeue(pod, seen)
                 continue
             self.stats["scheduled"] += 1
-            self._bound[md.get("uid", "")] = (md.get("namespace", "default"), md["name"])
+            self._bound[md.get("uid", "")] = (md.get("namespace", "default"), md["name"], node)
             if self.on_bound:
                 self.on_bound(pod, node, time.perf_counter())
-
-    def _requeue_bind(self, pod, node, seen):
-        def later():
-            time.sleep(self.retry)
-            if not self._stop.is_set():
-                self._bind_q.put((pod, node, seen))
-        threading.Thread(target=later, daemon=True).start()

@@ -10,6 +10,7 @@
 #include "extender_scan.h"
 #include "hal.h"
 #include "histogram.h"
+#include "http_client.h"
 #include "http_server.h"
 #include "platform.h"
 
@@ -582,4 +583,48 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("parked", [](PyHttpServer& s) { return s.srv->parked(); })
       .def("stats_json", [](PyHttpServer& s) { return s.srv->stats_json(); },
            py::call_guard<py::gil_scoped_release>());
+
+  // Keep-alive extender client of the scheduler stand-in.  `parts` are bytes
+  // objects sent back to back as the body (no join); the GIL is released for
+  // the round trip.  post() -> (status, bytes); post_names() -> (status, names
+  // of the Node items / nodenames in the reply) without building the reply in
+  // Python.
+  py::class_<HttpClient>(m, "HttpClient")
+      .def(py::init<std::string, int, double>(), py::arg("host"), py::arg("port"), py::arg("timeout_s") = 30.0)
+      .def("post", [](HttpClient& c, const std::string& path, const py::list& parts) {
+        std::vector<std::string_view> views;
+        for (const auto& h : parts) {
+          char* p = nullptr;
+          Py_ssize_t n = 0;
+          if (PyBytes_AsStringAndSize(h.ptr(), &p, &n) != 0) throw py::error_already_set();
+          views.emplace_back(p, static_cast<size_t>(n));
+        }
+        std::string body;
+        int status;
+        {
+          py::gil_scoped_release nogil;
+          status = c.post(path, views, &body);
+        }
+        return py::make_tuple(status, py::bytes(body));
+      })
+      .def("post_names", [](HttpClient& c, const std::string& path, const py::list& parts) {
+        std::vector<std::string_view> views;
+        for (const auto& h : parts) {
+          char* p = nullptr;
+          Py_ssize_t n = 0;
+          if (PyBytes_AsStringAndSize(h.ptr(), &p, &n) != 0) throw py::error_already_set();
+          views.emplace_back(p, static_cast<size_t>(n));
+        }
+        std::string body;
+        std::vector<std::string> names;
+        int status;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          status = c.post(path, views, &body);
+          ok = scan_node_names(body, &names);
+        }
+        if (!ok) throw std::runtime_error("reply is not an ExtenderFilterResult: " + body.substr(0, 200));
+        return py::make_tuple(status, names);
+      });
 }

@@ -430,6 +430,10 @@ void ExtenderHttpServer::on_readable(const ConnPtr& c) {
     if (full) {
       requests_.fetch_add(1, std::memory_order_relaxed);
       if (!dispatch(c, req, mono_ns())) return;  // parked: whoever finishes it continues
+      if (req.body.capacity() > c->body.capacity()) {  // keep the (multi-MB) buffer for the next request
+        req.body.clear();
+        c->body.swap(req.body);
+      }
       if (!c->keep_alive || c->dead) {
         close_conn(c);
         return;

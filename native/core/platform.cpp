@@ -295,7 +295,10 @@ std::string Platform::filter(const std::string& body) {
   // request's own bytes).
   auto reply = [&]() {
     std::string out;
-    out.reserve(64 + names.size() * 48);
+    // Full Node objects come back byte for byte: the reply is about as long
+    // as the request (growing a multi-megabyte string by doubling re-copies
+    // and re-faults it several times).
+    out.reserve(scan.have_nodes ? body.size() + 256 : 64 + names.size() * 48);
     out += "{\"failedNodes\":{";
     bool first = true;
     for (size_t i = 0; i < names.size(); ++i)
@@ -447,13 +450,32 @@ std::string Platform::preempt(const std::string& body) {
   for (const auto& kv : field(args, "nodeNameToVictims", "NodeNameToVictims").fields())
     if (std::find(names.begin(), names.end(), kv.first) == names.end()) names.push_back(kv.first);
   Json res = Json::object();
+  const int64_t now = now_ns();
   for (const auto& kv : sched_->preemption_plans(w, names)) {
+    // kube-scheduler resolves MetaVictims against the named node's own pods
+    // and fails the whole preemption if one is not there, so only victims ON
+    // the node are named.  A victim gang's members on other nodes are kept as
+    // that victim's peers: when the victim is released (evicted), release()
+    // hands them to the controller, which evicts the rest of the gang.
     Json mv = Json::object();
     Json pods = Json::array();
+    std::vector<std::string> here, elsewhere;
     for (const auto& uid : kv.second) {
+      Allocation a;
+      if (sched_->allocation(uid, &a) && a.node != kv.first) elsewhere.push_back(uid);
+      else here.push_back(uid);
+    }
+    if (here.empty() && !kv.second.empty()) continue;  // nothing evictable on this node itself
+    for (const auto& uid : here) {
       Json p = Json::object();
       p["uid"] = uid;
       pods.push_back(p);
+    }
+    if (!elsewhere.empty()) {
+      std::lock_guard<std::mutex> lk(pods_mu_);
+      for (const auto& uid : here) gang_peers_[uid] = {elsewhere, now};
+      for (auto it = gang_peers_.begin(); it != gang_peers_.end();)  // plans never acted on
+        it = now - it->second.second > 300LL * 1000000000 ? gang_peers_.erase(it) : std::next(it);
     }
     mv["pods"] = pods;
     mv["numPDBViolations"] = static_cast<int64_t>(0);
@@ -633,6 +655,23 @@ std::string Platform::release(const std::string& uid, double now_s) {
   UsageRecord r;
   Json out = Json::object();
   out["released"] = ok;
+  {
+    // A preemption victim whose gang has members on other nodes: they are
+    // the controller's to evict (see preempt()).
+    std::vector<std::string> peers;
+    {
+      std::lock_guard<std::mutex> lk(pods_mu_);
+      auto it = gang_peers_.find(uid);
+      if (it != gang_peers_.end()) {
+        if (now_ns() - it->second.second < 120LL * 1000000000) peers = it->second.first;
+        gang_peers_.erase(it);
+      }
+    }
+    Json pj = Json::array();
+    for (const auto& p : peers)
+      if (sched_->allocation(p, nullptr)) pj.push_back(p);
+    if (pj.size()) out["evict_gang_peers"] = pj;
+  }
   if (cost_->finalize(uid, now_s, &r)) {
     out["cost"] = to_json(r);
     reg_->observe("kgwe_workload_duration_seconds", {to_string(a.type)}, r.duration_s);

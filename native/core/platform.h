@@ -125,6 +125,8 @@ class Platform {
   // uid -> (monotonic first-seen ns, wall-clock creation stamp or 0) for
   // pods not yet bound: the latency origin and the queue.
   std::map<std::string, std::pair<int64_t, double>> pending_;
+  // preempt(): victim uid -> (its gang's members on other nodes, plan time).
+  std::map<std::string, std::pair<std::vector<std::string>, int64_t>> gang_peers_;
   LatencyHistogram pod_latency_;
   // tick() refreshes gauges at most at a 10 % duty cycle: at 10,000 GPUs a
   // refresh is ~0.5 s of CPU, and a scrape refreshes them anyway.
