@@ -61,6 +61,10 @@ _SIGS = {
     "kgwe_decode_argmax_finish": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "kgwe_decode_argmax_slots": (c_int, [c_int, c_int, c_int]),
     "kgwe_adamw_tensor_bytes": (c_int, []),
+    "kgwe_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                c_int, c_int, c_int, c_int, c_void_p]),
+    "kgwe_wgrad_splits": (c_int, [c_int, c_int, c_int]),
+    "kgwe_wgrad_workspace": (c_int64, [c_int, c_int, c_int]),
 }
 _OPTIONAL_SIGS = {
     "kgwe_flash_attn_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -6,10 +6,13 @@ PyTorch reference path (CPU tensors only).  Shapes follow the Llama block in
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
 from ._lib import check, lib, ptr, stream, use_hip
+from .gemm import wgrad, wgrad_supported
 
 
 def _require(cond: bool, msg: str) -> None:
@@ -232,6 +235,12 @@ def transpose(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     return out
 
 
+def _wgrad_mode() -> str:
+    mode = os.environ.get("KGWE_WGRAD", "auto")
+    _require(mode in ("auto", "kernel", "library"), "KGWE_WGRAD must be auto, kernel or library")
+    return mode
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T.  Forward is the plain library GEMM ("nt"); the input
     gradient uses the weight's persistent transposed copy when one exists
@@ -240,7 +249,13 @@ class _Linear(torch.autograd.Function):
     dimension of both stored operands, the slowest hipBLASLt layout on MI355X
     — is issued after transposing the SMALLER of X / dY, which moves it to
     the "tt" / "nn" kernels (tools/gemm_layouts.py: ~1.35 vs ~1.1 PF/s for
-    the Llama-3-8B shapes; the transpose of a [T, 4096] operand costs ~25 us)."""
+    the Llama-3-8B shapes; the transpose of a [T, 4096] operand costs ~25 us).
+
+    Where the library would need dY itself transposed (N < K, the MLP down
+    projection) the hand-written MFMA kernel of kgwe.ops.gemm takes both
+    operands as stored and is the faster of the two (1.70 vs 1.82 ms at
+    [4096, 14336] over 16,384 tokens); ``KGWE_WGRAD=kernel`` uses it for every
+    shape it supports, ``KGWE_WGRAD=library`` never."""
 
     @staticmethod
     def forward(ctx, x, w):
@@ -263,7 +278,10 @@ class _Linear(torch.autograd.Function):
             wt = ctx.wt
             dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(x.shape)
         if ctx.needs_input_grad[1]:
-            if x2.shape[0] % 8 or N % 8 or K % 8 or not x2.is_contiguous():
+            mode = _wgrad_mode()
+            if mode != "library" and (N < K or mode == "kernel") and wgrad_supported(dy2, x2):
+                dw = wgrad(dy2, x2)
+            elif x2.shape[0] % 8 or N % 8 or K % 8 or not x2.is_contiguous():
                 dw = torch.mm(dy2.t(), x2)
             elif N >= K:
                 dw = torch.mm(dy2.t(), transpose(x2).t())   # "tt"

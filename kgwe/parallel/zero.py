@@ -109,14 +109,11 @@ class ShardedDataParallel:
         if not params:
             raise ValueError("ShardedDataParallel: model has no trainable parameters")
         self.device = params[0].device
-        # Side stream of the optimizer update, at HIGH priority (-1; torch
-        # clamps to the device's range, (0, -1) on MI355X): the update's
-        # workgroups are dispatched ahead of the backward GEMM's, so each
-        # bucket's HBM-bound burst finishes sooner and overlaps less GEMM time
-        # — 701.4 vs 706.7 ms/step at normal priority (Llama-3-8B, one GPU,
-        # tools/gpu_side_prio.sh).  KGWE_SIDE_PRIORITY overrides.
-        prio = int(os.environ.get("KGWE_SIDE_PRIORITY", "-1"))
-        self._side = (torch.cuda.Stream(self.device, priority=prio)
+        # Side stream of the optimizer update, at the DEFAULT priority like
+        # every other stream of the process: work on streams of different
+        # priorities has hung on MI355X hosts (a high-priority update stream
+        # measured ~5 ms/step faster, 701 vs 707 ms; not worth a hang).
+        self._side = (torch.cuda.Stream(self.device)
                       if self.device.type == "cuda" and (self.overlap or self.world > 1) else None)
         self.buckets: list[_Bucket] = []
         bucket_elems = int(os.environ.get("KGWE_BUCKET_MELEMS", "0")) * 2**20 or bucket_elems

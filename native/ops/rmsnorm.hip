@@ -231,6 +231,13 @@ KGWE_API int kgwe_rmsnorm_fwd(const void* x, const void* res, const void* w,
   }
 }
 
+namespace {
+__global__ void zero_f32_kernel(float* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0.0f;
+}
+}  // namespace
+
 KGWE_API int kgwe_rmsnorm_bwd(const void* dy, const void* h, const void* w,
                               const float* rstd, const void* dadd, void* dx,
                               float* partial, void* dw_bf16, float* dw_f32,
@@ -242,7 +249,10 @@ KGWE_API int kgwe_rmsnorm_bwd(const void* dy, const void* h, const void* w,
   auto DA = static_cast<const bf16_t*>(dadd);
   auto DX = static_cast<bf16_t*>(dx);
   // `partial` is the fp32 dw accumulator, at least H floats.
-  if (hipMemsetAsync(partial, 0, static_cast<size_t>(H) * sizeof(float), s) != hipSuccess) return -2;
+  // Cleared by a kernel, not hipMemsetAsync: memset nodes recorded into a
+  // captured graph have replayed wrongly on this platform.
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((H + 255) / 256), dim3(256), 0, s, partial, H);
+  if (KGWE_CHECK_LAUNCH()) return -2;
   int rc;
   switch (H) {
     case 512: rc = launch_bwd<1>(DY, Hh, W, rstd, DA, DX, partial, G, T, H, s); break;

@@ -61,6 +61,28 @@ def test_bench_gpus4_rehearses_the_multi_rank_path():
     assert rr.get("grad_reduce_dtype") == "bf16" or "error" in rr, rr
 
 
+def test_bench_gpus8_rehearses_the_drivers_headline_point():
+    """Eight gloo ranks (the driver's N=8 point, the BASELINE config's rank
+    count): headline row, reduce-dtype row and FSDP2 row all run, every rank
+    reports its own loss, and the job-wide token rate is the sum over ranks."""
+    r, lines = _run(8, ["--model", "tiny", "--seq-len", "64", "--micro-batch", "1",
+                        "--fsdp-row", "on", "--reduce-row", "on"], timeout=600,
+                    env_extra={"OMP_NUM_THREADS": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "zero2-dp8"
+    assert out["config"]["global_batch"] == 8 and out["scaling"] == "weak"
+    assert len(out["loss_per_rank"]) == 8 and len(set(out["loss_per_rank"])) == 8
+    assert len(out["util_per_rank"]) == 8
+    assert out["fsdp_row"]["parallelism"] == "fsdp8" and "error" not in out["fsdp_row"]
+    rr = out["reduce_dtype_row"]
+    assert rr.get("grad_reduce_dtype") == "bf16" or "error" in rr, rr
+    # whole-job rate: 8 ranks x 64 tokens per step
+    assert abs(out["tokens_per_s"] - 8 * 64 / (out["ms_per_step"] / 1e3)) < 0.02 * out["tokens_per_s"]
+    assert abs(out["tokens_per_s_per_gpu"] * 8 - out["tokens_per_s"]) < 0.02 * out["tokens_per_s"]
+
+
 def test_bench_failing_rank_fails_the_launcher():
     # An impossible model name makes every rank raise: the launcher must exit
     # non-zero and print no result line.

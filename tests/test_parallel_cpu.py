@@ -33,21 +33,36 @@ def _batches(world: int):
     return [torch.randint(0, 1024, (world, 65), generator=g) for _ in range(STEPS)]
 
 
-def _model():
+def _model(odd: bool = False):
+    """odd=True adds two parameters of 37 and 1001 elements (used through
+    ``_loss``), so bucket sizes stop being multiples of the shard alignment."""
     torch.manual_seed(0)
-    return llama.build("tiny", device="cpu", dtype=torch.float32)
+    m = llama.build("tiny", device="cpu", dtype=torch.float32)
+    if odd:
+        m.extra_a = torch.nn.Parameter(torch.randn(37))
+        m.extra_b = torch.nn.Parameter(torch.randn(7, 143))
+    return m
 
 
-def _rank_main(rank, world, port, out, bucket_elems, overlap=True):
+def _loss(m, inp, tgt):
+    loss = m(inp, tgt)
+    if hasattr(m, "extra_a"):
+        loss = loss + 0.01 * (m.extra_a.float().square().sum() + m.extra_b.float().square().sum())
+    return loss
+
+
+def _rank_main(rank, world, port, out, bucket_elems, overlap=True, reduce_dtype="fp32", odd=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)  # up to 8 ranks share this host's cores
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        m = _model()
-        dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems, overlap_step=overlap)
+        m = _model(odd)
+        dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems, overlap_step=overlap,
+                                 reduce_dtype=torch.bfloat16 if reduce_dtype == "bf16" else torch.float32)
         losses = []
         for tok in _batches(world):
             mine = tok[rank:rank + 1]
-            loss = m(mine[:, :-1], mine[:, 1:])
+            loss = _loss(m, mine[:, :-1], mine[:, 1:])
             loss.backward()
             dp.step()
             losses.append(loss.item())
@@ -55,19 +70,20 @@ def _rank_main(rank, world, port, out, bucket_elems, overlap=True):
         torch.save({"params": {k: v.detach().clone() for k, v in m.named_parameters()},
                     "master": [b.master.clone() for b in dp.buckets],
                     "numel": [b.numel for b in dp.buckets],
+                    "padded": [b.padded for b in dp.buckets], "shard": [b.shard for b in dp.buckets],
                     "losses": losses, "nbuckets": len(dp.buckets)}, f"{out}/rank{rank}.pt")
     finally:
         dist.destroy_process_group()
 
 
-def _single_process_reference(world, bucket_elems):
-    m = _model()
+def _single_process_reference(world, bucket_elems, odd=False):
+    m = _model(odd)
     # overlap off: the update runs in step(), after backward — the plain
     # ordering the overlapped (in-hook) path must reproduce
     dp = ShardedDataParallel(m, lr=LR, bucket_elems=bucket_elems, overlap_step=False)
     assert dp.world == 1
     for tok in _batches(world):
-        loss = m(tok[:, :-1], tok[:, 1:])  # mean over both ranks' tokens
+        loss = _loss(m, tok[:, :-1], tok[:, 1:])  # mean over both ranks' tokens
         loss.backward()
         dp.step()
     return ({k: v.detach().clone() for k, v in m.named_parameters()},
@@ -170,3 +186,57 @@ def test_busbw_sweep_world2_on_caller_group(tmp_path):
     mp.spawn(_busbw_rank, args=(2, _port(), out), nprocs=2, join=True)
     r = torch.load(out, weights_only=True)
     assert r["ndev"] == 2 and r["n"] == 2 and r["peak"] > 0
+
+
+# Ragged bucket size: buckets end at odd element counts, so every bucket is
+# padded up to the world * 64 shard alignment and the last shards hold padding.
+RAGGED = 300_001
+
+
+def _run_world(tmp_path, world, reduce_dtype):
+    out = tmp_path / f"w{world}-{reduce_dtype}"
+    out.mkdir()
+    mp.spawn(_rank_main, args=(world, _port(), str(out), RAGGED, True, reduce_dtype, True), nprocs=world,
+             join=True)
+    return [torch.load(out / f"rank{r}.pt", weights_only=True) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_dp_world4_and_8_match_single_process_for_both_reduce_dtypes(tmp_path, world):
+    """Worlds 4 and 8 (the driver's scaling points) against ONE process that
+    sees all ranks' batches, with ragged buckets, for the fp32 and the bf16
+    gradient reduce-scatter; and the bf16 reduce bounded against the fp32 one.
+    Adam's update is ~lr * sign(g) early on, so a reduction that is wrong (a
+    missing rank, a misplaced shard, padding mixed in) moves a large share of
+    the elements by ~lr per step; rounding differences move only elements
+    whose gradient is near zero."""
+    ref, ref_master = _single_process_reference(world, RAGGED, odd=True)
+    res = {}
+    for rd in ("fp32", "bf16"):
+        ranks = _run_world(tmp_path, world, rd)
+        r0 = ranks[0]
+        assert r0["nbuckets"] > 2
+        for n, padded, shard in zip(r0["numel"], r0["padded"], r0["shard"]):
+            assert padded % (world * 64) == 0 and shard * world == padded and padded - n < world * 64
+        assert any(p != n for p, n in zip(r0["padded"], r0["numel"]))  # padding is exercised
+        for k in ref:  # replicas are bit-identical after the all-gather
+            for r in ranks[1:]:
+                assert torch.equal(r0["params"][k], r["params"][k]), (rd, k)
+        masters = []
+        for i, (n, want) in enumerate(zip(r0["numel"], ref_master)):
+            got = torch.cat([r["master"][i] for r in ranks])[:n]
+            masters.append(got)
+            d = (got - want).abs()
+            assert d.mean().item() < 0.03 * LR * STEPS, (rd, i, d.mean().item())
+            assert (d > 0.5 * LR).float().mean().item() < 0.02, (rd, i)
+        assert len({tuple(r["losses"]) for r in ranks}) == world  # every rank saw its own data
+        res[rd] = masters
+    # bf16 reduce against fp32 reduce: same order of difference as either
+    # against the single process — halving the xGMI bytes costs no accuracy
+    # beyond the bf16 rounding of the gradients themselves.
+    worst = 0.0
+    for a, b in zip(res["fp32"], res["bf16"]):
+        d = (a - b).abs()
+        worst = max(worst, d.mean().item())
+        assert (d > 0.5 * LR).float().mean().item() < 0.02
+    assert worst < 0.03 * LR * STEPS, worst
