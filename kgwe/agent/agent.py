@@ -140,8 +140,11 @@ class NodeAgent:
             body = dict(self.topology)
             if self.cfg.get("advertise"):  # where the controller reaches this agent's gRPC
                 body["agent_endpoint"] = self.cfg["advertise"]
-            c.request("POST", f"/v1/nodes/{self.name}/topology", body=json.dumps(body),
-                      headers={"Content-Type": "application/json"})
+            headers = {"Content-Type": "application/json"}
+            tok = self._token()
+            if tok:  # the controller only accepts an advertised endpoint from an authenticated push
+                headers["Authorization"] = "Bearer " + tok
+            c.request("POST", f"/v1/nodes/{self.name}/topology", body=json.dumps(body), headers=headers)
             ok = c.getresponse().status == 200
         except OSError:
             ok = False

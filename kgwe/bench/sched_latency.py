@@ -56,7 +56,7 @@ MIX = [  # (weight, kind, gpus)
 ]
 
 
-def _pod(name: str, kind: str, gpus: int, priority: int) -> dict:
+def _pod(name: str, kind: str, gpus: int, priority: int, preemptible: bool = True) -> dict:
     from ..controller.schedsim import SCHEDULER_NAME
 
     ann = {"kgwe.amd.com/topology": "xGMIOptimal" if gpus > 1 else "None",
@@ -65,6 +65,8 @@ def _pod(name: str, kind: str, gpus: int, priority: int) -> dict:
            "kgwe.amd.com/created-at": f"{time.time():.6f}"}
     if kind == "fsdp":
         ann["kgwe.amd.com/strategy"] = "FSDP"
+    if not preemptible:
+        ann["kgwe.amd.com/preemptible"] = "false"
     res = {"amd.com/gpu-cpx": "1"} if kind == "cpx" else {"amd.com/gpu": str(gpus)}
     return {"apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": name, "namespace": "bench", "annotations": ann,
@@ -147,7 +149,7 @@ def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev, ready_ev, node
 
 
 def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s: float,
-                     reclaim_idle_s: float, parent_api=None):
+                     reclaim_idle_s: float, parent_api=None, mean_lifetime_s: float = 0.0):
     """The kgwe controller: ExtenderServer on the C++ core plus its periodic
     housekeeping, alone in its process as in production (the load driver's
     threads must not share its GIL).  Commands over `conn`:
@@ -163,7 +165,14 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
     # Housekeeping as the controller runs it (tick: gang expiry, cost sampling,
     # idle-partition reclaim).  Pod lifetimes here are seconds, not hours, so
     # the reclaim hysteresis is scaled down with them (production default 60 s).
-    plat = Platform({"enforceBudgets": True, "partitionReclaimIdleSeconds": reclaim_idle_s})
+    # Likewise the preemption policy's clocks: production waits for jobs within
+    # 30 s of their expected end (of hours); here within a fifth of the mean
+    # lifetime, for at most one mean lifetime.  Lifetimes are not declared by
+    # the pods: the scheduler learns them per workload type from releases.
+    sched_cfg = ({"preemptionWaitWindowSeconds": 0.2 * mean_lifetime_s,
+                  "preemptionMaxWaitSeconds": mean_lifetime_s} if mean_lifetime_s > 0 else {})
+    plat = Platform({"enforceBudgets": True, "partitionReclaimIdleSeconds": reclaim_idle_s,
+                     "scheduler": sched_cfg})
     for i in range(n_nodes):
         name = f"mi355x-{i:03d}"
         plat.add_fake_node(make_fixture(name, 8, 2))
@@ -180,13 +189,8 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
     slice_util: list[float] = []
     queue_depth: list[int] = []
 
-    _no = os.environ.get("KGWE_BENCH_NO", "")
-
     def partition_sampler():  # time-average of CPX/QPX/DPX slice occupancy
         while not done.is_set():
-            if "sampler" in _no:
-                time.sleep(0.1)
-                continue
             m = plat.partition_metrics()
             if any(k != "SPX" and v.get("gpus", 0) for k, v in m.get("modes", {}).items()):
                 slice_util.append(m.get("slice_utilization", 0.0))
@@ -194,10 +198,8 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
 
     def housekeeping():
         while not done.is_set():
-            if "tick" not in _no:
-                plat.tick()
-            if "consolidate" not in _no:
-                plat.consolidate_partitions(plan_only=False)  # the controller's consolidation (ledger move)
+            plat.tick()
+            plat.consolidate_partitions(plan_only=False)  # the controller's consolidation (ledger move)
             queue_depth.append(plat.queue_depth())
             time.sleep(tick_s)
 
@@ -232,6 +234,8 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
                                                     if slice_util else None),
                 "partition_slice_samples": len(slice_util),
                 "topology_optimal_placements": sm.get("topology_optimal", 0),
+                "preemptions_deferred_wait": sm.get("preemptions_deferred_wait", 0),
+                "preemptions_rate_limited": sm.get("preemptions_rate_limited", 0),
                 "extender_phases_ms": ext.phase_summary(),
                 "extender_server": {k: v for k, v in ext.stats().items() if k != "verbs"},
             })
@@ -255,7 +259,8 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
     kube = KubeClient(api_url)
     ctl, ctl_child = ctx.Pipe()
     ctl_p = ctx.Process(target=_controller_proc, args=(ctl_child, api_url, n_nodes, full_nodes, tick_s,
-                                                       reclaim_idle_s, parent), daemon=True)
+                                                       reclaim_idle_s, parent, 0.5 * sum(lifetime_s)),
+                        daemon=True)
     ctl_p.start()
     ext_url = ctl.recv()
     ctl_lock = threading.Lock()
@@ -297,6 +302,7 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
                 continue
             with lock:
                 t0 = created.pop(name, None)
+                name_of[uid] = name
                 n_bound[0] += 1
                 finished = n_bound[0] >= n_pods + 1
             if t0 is not None:  # the harness's own clock; bind() feeds the product's histogram
@@ -329,6 +335,8 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
             time.sleep(0.01)
 
     expiry: list = []
+    protected: set[str] = set()
+    name_of: dict[str, str] = {}
     threading.Thread(target=consumer, daemon=True).start()
     threading.Thread(target=reaper, daemon=True).start()
     time.sleep(0.3)  # scheduler process: first watch established
@@ -347,9 +355,13 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
             time.sleep(delay)
         with lock:
             created[name] = time.perf_counter()
-        # priority classes: 90 % best effort (0), 8 % production (100), 2 % critical (1000)
+        # priority classes: 90 % best effort (0), 8 % production (100), 2 % critical (1000);
+        # a fifth of the best-effort pods declare themselves non-preemptible
         pr = rnd.random()
-        kube.create_pod(_pod(name, kind, g, 0 if pr < 0.90 else 100 if pr < 0.98 else 1000))
+        keep = pr < 0.90 and rnd.random() < 0.2
+        if keep:
+            protected.add(name)
+        kube.create_pod(_pod(name, kind, g, 0 if pr < 0.90 else 100 if pr < 0.98 else 1000, not keep))
     all_done.wait(timeout=timeout_s)
     wall = time.perf_counter() - t_start
     stop_ev.set()
@@ -386,6 +398,8 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
         "preemptions": len(preempted),
         "preemption_rate_pct": round(100.0 * len(preempted) / max(1, n_bound[0]), 3),
         "preempt_verb_calls": sim_stats.get("preempt_calls"),
+        "non_preemptible_pods": len(protected),
+        "non_preemptible_evicted": sum(1 for v in preempted if name_of.get(v, v) in protected),
         "first_cycle_breakdown_ms": {k: {"p50": round(h.quantile_ms(0.5), 3), "p99": round(h.quantile_ms(0.99), 3)}
                                      for k, h in phase.items()},
         "scheduler_round_trips_ms": {k[:-6]: v for k, v in sim_stats.items() if k.endswith("_rt_ms")},

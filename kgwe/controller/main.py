@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import argparse
+import hmac
 import json
 import signal
 import sys
@@ -29,7 +30,10 @@ DEFAULTS = {
     "kube": {"url": "", "inCluster": False, "insecure": False},
     "scheduler": {"topologyWeight": 40, "resourceWeight": 35, "balanceWeight": 25,
                   "enablePreemption": True, "enableGangScheduling": True, "gangTimeoutMs": 30000,
-                  "maxSchedulingAttempts": 3, "scoring": "xgmi", "placement": "pack"},
+                  "maxSchedulingAttempts": 3, "scoring": "xgmi", "placement": "pack",
+                  "preemptionCandidateNodes": 8, "preemptionWaitWindowSeconds": 30.0,
+                  "preemptionMaxWaitSeconds": 120.0, "preemptionUrgentPriority": 1000000,
+                  "preemptionMaxRatePercent": 4.0, "preemptionWindowSeconds": 300, "preemptionBurst": 8},
     "webhook": {"port": 8443, "certFile": "", "keyFile": ""},
     "cost": {"journalPath": "", "enableSpotOptimization": True, "enableRightsizing": True},
     "partitionDryRun": False,
@@ -42,6 +46,10 @@ DEFAULTS = {
     "partitionConsolidateAfterSeconds": 120.0,
     "migrationCooldownSeconds": 3600.0,
     "agentActuation": {"enabled": True, "tokenFile": "/etc/kgwe/actuation/token", "timeoutSeconds": 30.0},
+    # Node-agent pushes: with the actuation token configured they must carry it,
+    # and an agent's advertised endpoint (which later receives that token) must
+    # be an address of the Node object it claims to be.
+    "agentPush": {"requireToken": True, "pinEndpointToNode": True},
     "fakeNodes": 0,
     "labelNodes": True,
     "tickSeconds": 5.0,
@@ -97,26 +105,65 @@ def build(cfg: dict):
     if cfg["agentActuation"]["enabled"]:
         plat.set_partition_actuator(actuate)
 
-    def agent_push(path, body):
+    node_addrs: dict[str, tuple[float, set]] = {}  # node -> (fetched at, addresses of its Node object)
+
+    def addresses_of(name: str) -> set | None:
+        """The Node object's own addresses (InternalIP, Hostname, ...), cached
+        for a minute; None when there is no apiserver to ask."""
+        if kube is None:
+            return None
+        hit = node_addrs.get(name)
+        if hit and time.time() - hit[0] < 60.0:
+            return hit[1]
+        try:
+            obj = kube.get_node(name)
+            addrs = {a.get("address", "") for a in (obj.get("status") or {}).get("addresses") or []}
+        except Exception:  # noqa: BLE001 - unknown node: nothing is pinned to it
+            addrs = set()
+        node_addrs[name] = (time.time(), addrs)
+        return addrs
+
+    def agent_push(path, body, authorization=""):
+        """Topology push of a node agent.  With a token configured the push
+        must carry it (401 otherwise), and only then may it name the endpoint
+        the controller later sends that same token to; with an apiserver the
+        endpoint's host must also be one of the Node object's addresses.  No
+        token configured (development): topology is accepted, endpoints are
+        not."""
         node = json.loads(body)
         name = path.rstrip("/").split("/")[-2]  # /v1/nodes/<name>/topology
         node["name"] = name
-        if node.get("agent_endpoint"):
-            endpoints[name] = node["agent_endpoint"]
+        want = token()
+        got = authorization[7:] if authorization.startswith("Bearer ") else ""
+        authed = bool(want) and hmac.compare_digest(got.encode(), want.encode())
+        if want and not authed and cfg["agentPush"]["requireToken"]:
+            return 401, b'{"error":"unauthorized: node agent pushes carry the actuation token"}'
+        ep = node.pop("agent_endpoint", "")
+        note = {}
+        if ep:
+            host = ep.rsplit(":", 1)[0].strip("[]")
+            addrs = addresses_of(name)
+            if not authed:
+                note["endpointIgnored"] = "push not authenticated"
+            elif addrs is not None and host not in addrs and cfg["agentPush"]["pinEndpointToNode"]:
+                note["endpointIgnored"] = f"{host} is not an address of Node {name}"
+            else:
+                endpoints[name] = ep
         plat.upsert_node(node)
         if labeler is not None:
             try:
                 labeler.update(name, node)
             except Exception as e:  # noqa: BLE001 - labels are advisory; keep the topology
                 return 200, json.dumps({"ok": True, "labelError": str(e)}).encode()
-        return 200, b'{"ok":true}'
+        return 200, json.dumps(dict({"ok": True}, **note)).encode()
 
     def admission(path, body):
         return 200, json.dumps(webhook.review(json.loads(body), mutate=path.startswith("/mutate"))).encode()
 
     ext = ExtenderServer(plat, kube=kube, host=cfg["listen"]["host"], port=int(cfg["listen"]["port"]),
                          url_prefix=cfg["listen"]["urlPrefix"],
-                         routes={"/v1/nodes/": agent_push, "/validate": admission, "/mutate": admission})
+                         routes={"/v1/nodes/": agent_push, "/validate": admission, "/mutate": admission},
+                         auth_routes={"/v1/nodes/"})
     optimizer = None
     if cfg["optimizer"]["target"]:  # the optimizer Deployment (gRPC :50051)
         from ..optimizer.server import OptimizerClient  # noqa: PLC0415

@@ -192,6 +192,11 @@ class Platform:
         caller evicts the moved pods; False: the ledger moves them itself."""
         return _j(self._p.consolidate_partitions(time.time() if now is None else now, plan_only))
 
+    def draining_gpus(self) -> list:
+        """Consolidation donors that take no new slice work until they are
+        empty and switched back to SPX."""
+        return list(self._p.draining_gpus())
+
     def pod_latency_quantile_ms(self, q: float) -> float:
         """Pod create -> bind latency quantile recorded by bind() itself."""
         return self._p.pod_latency_quantile_ms(q)

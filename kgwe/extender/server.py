@@ -70,10 +70,11 @@ class ExtenderServer:
 
     def __init__(self, platform: Platform, kube=None, host: str = "0.0.0.0", port: int = 8080,
                  url_prefix: str = "", routes: dict | None = None, workers: int = 0,
-                 gang_hold_s: float = 25.0):
+                 gang_hold_s: float = 25.0, auth_routes=()):
         """routes: extra POST handlers {path_prefix: fn(path, body) -> (code, bytes)}
         (the controller mounts the admission webhook and the node-agent push
-        endpoint here).  gang_hold_s: how long a gang member's bind request is
+        endpoint here); a prefix also listed in auth_routes is called as
+        fn(path, body, authorization_header).  gang_hold_s: how long a gang member's bind request is
         held for the rest of its gang before it is answered with a retryable
         error (keep it below the scheduler's extender httpTimeout, 30 s in the
         reference's profile); 0 answers at once, as an extender without Permit
@@ -85,6 +86,7 @@ class ExtenderServer:
         self.host = host
         self.prefix = url_prefix.rstrip("/")
         self.routes = dict(routes or {})
+        self.auth_routes = set(auth_routes or ())
         self._ready = lambda: True
         self._tracer = tracing.PhaseTimer()
         self._srv = native.HttpServer(platform.raw, host, int(port), self.prefix, int(workers),
@@ -172,9 +174,10 @@ class ExtenderServer:
         # (the pod is never seen bound without its placement, or the reverse)
         self.kube.bind_pod(ns, name, node, uid, annotations=ann)
 
-    def _fallback(self, method: str, path: str, raw: bytes):
+    def _fallback(self, method: str, path: str, raw: bytes, authorization: str = ""):
         """(code, body, content type) for every request the native server does
-        not answer itself."""
+        not answer itself.  Routes registered with ``auth_routes`` get the
+        request's Authorization header as a third argument."""
         if method == "GET":
             if path == "/debug/allocations":
                 return 200, json.dumps(self.platform.allocations()).encode(), "application/json"
@@ -198,7 +201,8 @@ class ExtenderServer:
         for pre, fn in self.routes.items():
             if path.startswith(pre):
                 try:
-                    code, data = fn(path, body)
+                    code, data = (fn(path, body, authorization) if pre in self.auth_routes
+                                  else fn(path, body))
                 except Exception as e:  # noqa: BLE001
                     code, data = 500, json.dumps({"error": str(e)}).encode()
                 return code, data, "application/json"
@@ -242,7 +246,8 @@ class ExtenderServer:
             def _serve(self, method: str):
                 n = int(self.headers.get("Content-Length") or 0)
                 raw = self.rfile.read(n) if n else b"{}"
-                code, data, ctype = outer._fallback(method, self.path.split("?")[0], raw)
+                code, data, ctype = outer._fallback(method, self.path.split("?")[0], raw,
+                                                    self.headers.get("Authorization") or "")
                 self.send_response(code)
                 self.send_header("Content-Type", ctype)
                 self.send_header("Content-Length", str(len(data)))

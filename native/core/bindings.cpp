@@ -49,6 +49,16 @@ PlatformConfig config_from_json(const std::string& s) {
   c.consolidate.after_s = j.get("partitionConsolidateAfterSeconds").as_number(c.consolidate.after_s);
   c.consolidate.cooldown_s = j.get("migrationCooldownSeconds").as_number(c.consolidate.cooldown_s);
   c.sched.max_share_clients = static_cast<int>(sc.get("maxShareClients").as_int(c.sched.max_share_clients));
+  c.sched.preemption_candidate_nodes =
+      static_cast<int>(sc.get("preemptionCandidateNodes").as_int(c.sched.preemption_candidate_nodes));
+  c.sched.preemption_wait_window_s = sc.get("preemptionWaitWindowSeconds").as_number(c.sched.preemption_wait_window_s);
+  c.sched.preemption_max_wait_s = sc.get("preemptionMaxWaitSeconds").as_number(c.sched.preemption_max_wait_s);
+  c.sched.preemption_urgent_priority =
+      sc.get("preemptionUrgentPriority").as_int(c.sched.preemption_urgent_priority);
+  c.sched.preemption_max_rate_percent =
+      sc.get("preemptionMaxRatePercent").as_number(c.sched.preemption_max_rate_percent);
+  c.sched.preemption_window_s = static_cast<int>(sc.get("preemptionWindowSeconds").as_int(c.sched.preemption_window_s));
+  c.sched.preemption_burst = static_cast<int>(sc.get("preemptionBurst").as_int(c.sched.preemption_burst));
   c.sched.default_cu_percent = sc.get("defaultCuPercent").as_number(c.sched.default_cu_percent);
   return c;
 }
@@ -67,6 +77,8 @@ Json metrics_json(const SchedulerMetrics& m) {
   j["failed"] = m.failed;
   j["topology_optimal"] = m.topology_optimal;
   j["preemptions"] = m.preemptions;
+  j["preemptions_deferred_wait"] = m.preemptions_deferred_wait;
+  j["preemptions_rate_limited"] = m.preemptions_rate_limited;
   j["releases"] = m.releases;
   j["gang_timeouts"] = m.gang_timeouts;
   j["avg_latency_ms"] = m.avg_latency_ms;
@@ -160,7 +172,7 @@ struct PyHttpServer {
       HttpResponse r;
       py::gil_scoped_acquire g;
       try {
-        py::tuple t = h->fn(rq.method, rq.path, py::bytes(rq.body)).cast<py::tuple>();
+        py::tuple t = h->fn(rq.method, rq.path, py::bytes(rq.body), rq.authorization).cast<py::tuple>();
         r.code = t[0].cast<int>();
         r.body = t[1].cast<std::string>();
         if (t.size() > 2) r.ctype = t[2].cast<std::string>();
@@ -435,6 +447,7 @@ PYBIND11_MODULE(_kgwe_core, m) {
       .def("set_partition_actuator", [](PyPlatform& s, DiscoveryService::RemoteActuator fn) {
         s.p->discovery()->set_remote_actuator(std::move(fn));
       })
+      .def("draining_gpus", [](PyPlatform& s) { return s.p->scheduler()->draining(); })
       .def("consolidate_partitions", [](PyPlatform& s, double now, bool plan_only) {
         return s.p->consolidate_partitions(now, !plan_only);
       }, py::arg("now"), py::arg("plan_only") = true, py::call_guard<py::gil_scoped_release>())

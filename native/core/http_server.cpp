@@ -70,7 +70,7 @@ struct ExtenderHttpServer::Conn {
   // request being read
   std::string hdr;  // bytes up to the end of the headers (and whatever followed)
   bool have_hdr = false;
-  std::string method, target;
+  std::string method, target, authorization;
   bool keep_alive = true, chunked = false;
   size_t content_length = 0, body_got = 0;
   std::string body;
@@ -340,6 +340,7 @@ bool ExtenderHttpServer::parse(Conn& c, HttpRequest* req, bool* bad) {
     c.keep_alive = line.compare(s2 + 1, std::string::npos, "HTTP/1.0") != 0;
     c.chunked = false;
     c.content_length = 0;
+    c.authorization.clear();
     bool expect = false;
     size_t p = l0 + 2;
     while (p < end) {
@@ -359,6 +360,7 @@ bool ExtenderHttpServer::parse(Conn& c, HttpRequest* req, bool* bad) {
           if (lv.find("close") != std::string::npos) c.keep_alive = false;
           else if (lv.find("keep-alive") != std::string::npos) c.keep_alive = true;
         } else if (ieq(name, nlen, "expect")) expect = lower(val).find("100-continue") != std::string::npos;
+        else if (ieq(name, nlen, "authorization")) c.authorization = val;
       }
       p = e + 2;
     }
@@ -407,6 +409,7 @@ bool ExtenderHttpServer::parse(Conn& c, HttpRequest* req, bool* bad) {
   req->path = c.target.substr(0, q);
   req->query = q == std::string::npos ? "" : c.target.substr(q + 1);
   req->body = std::move(c.body);
+  req->authorization = c.authorization;
   c.body.clear();
   c.have_hdr = false;
   return true;

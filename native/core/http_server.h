@@ -38,6 +38,7 @@ namespace kgwe {
 
 struct HttpRequest {
   std::string method, path, query, body;
+  std::string authorization;  // the Authorization header's value, if any
 };
 
 struct HttpResponse {

@@ -237,6 +237,9 @@ void MetricRegistry::declare_kgwe_families() {
   declare("kgwe_scheduling_failures_total", M::Counter, "Failed placements", {"reason"});
   declare("kgwe_topology_optimal_placements_total", M::Counter, "Placements with topology score >= 80", {});
   declare("kgwe_preemptions_total", M::Counter, "Workloads preempted", {});
+  declare("kgwe_preemptions_deferred_total", M::Counter,
+          "Preemption requests not served: told to wait for a near completion (wait) or over the rate window (rate)",
+          {"reason"});
   // Devices
   declare("kgwe_gpu_count", M::Gauge, "GPUs discovered", {"node"});
   declare("kgwe_gpu_utilization_percent", M::Gauge, "GPU utilization (amd-smi gfx_activity %)",

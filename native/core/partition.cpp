@@ -426,20 +426,38 @@ std::vector<PartitionMove> PartitionController::consolidate(double now_s, const 
     std::lock_guard<std::mutex> lk(mu_);
     draining = draining_;
   }
+  // Until then the scheduler places no new slice work on them (plan-only
+  // callers evict the donor's pods; without the bar the same pods could be
+  // scheduled straight back).  A donor that has not emptied within the drain
+  // limit (its pods were never evicted) is given back.
+  const double drain_limit_s = std::max(300.0, 2.0 * pol.after_s);
+  auto undrain = [&](const std::string& uuid, const std::string& node) {
+    sched_->set_draining(uuid, node, false);
+    std::lock_guard<std::mutex> lk(mu_);
+    draining_.erase(uuid);
+    draining_since_.erase(uuid);
+  };
   for (const auto& uuid : draining) {
+    bool found = false;
     for (const auto& kv : snap->nodes)
       if (const GpuDevice* g = kv.second.gpu(uuid)) {
-        if (g->partition.compute == ComputePartition::SPX) {
+        found = true;
+        double since = now_s;
+        {
           std::lock_guard<std::mutex> lk(mu_);
-          draining_.erase(uuid);
+          auto it = draining_since_.find(uuid);
+          if (it != draining_since_.end()) since = it->second;
+        }
+        if (g->partition.compute == ComputePartition::SPX) {
+          undrain(uuid, kv.first);
         } else if (gpu_idle(*g)) {
           PartitionOp op = execute(kv.first, *g, ComputePartition::SPX, "consolidation: donor emptied", false);
-          if (op.state != OpState::Failed) {
-            std::lock_guard<std::mutex> lk(mu_);
-            draining_.erase(uuid);
-          }
+          if (op.state != OpState::Failed) undrain(uuid, kv.first);
+        } else if (now_s - since > drain_limit_s) {
+          undrain(uuid, kv.first);
         }
       }
+    if (!found) undrain(uuid, "");  // the GPU left the fleet
   }
   snap = disc_->snapshot();
   const auto allocs = sched_->allocations();
@@ -561,20 +579,21 @@ std::vector<PartitionMove> PartitionController::consolidate(double now_s, const 
     migrations_ += static_cast<int>(moves.size());
     for (const auto& u : emptied) {
       draining_.insert(u);
+      draining_since_[u] = now_s;
       low_since_.erase(u);
     }
     if (migrated_at_.size() > 100000) migrated_at_.clear();
   }
-  if (move_in_ledger) {  // donors are empty right now: switch them back
+  {
     auto s2 = disc_->snapshot();
     for (const auto& u : emptied)
       for (const auto& kv : s2->nodes)
         if (const GpuDevice* g = kv.second.gpu(u)) {
+          sched_->set_draining(u, kv.first, true);  // no new slice work on a donor
+          if (!move_in_ledger) continue;            // its pods are still to be evicted by the caller
+          // donors are empty right now: switch them back
           PartitionOp op = execute(kv.first, *g, ComputePartition::SPX, "consolidation: donor emptied", false);
-          if (op.state != OpState::Failed) {
-            std::lock_guard<std::mutex> lk(mu_);
-            draining_.erase(u);
-          }
+          if (op.state != OpState::Failed) undrain(u, kv.first);
         }
   }
   return moves;

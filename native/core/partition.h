@@ -151,6 +151,7 @@ class PartitionController {
   std::map<std::string, double> low_since_;   // partitioned GPU uuid -> first under-used tick
   std::map<std::string, double> migrated_at_; // workload uid -> last migration
   std::set<std::string> draining_;            // donors emptied by consolidation
+  std::map<std::string, double> draining_since_;
   int migrations_ = 0;
   std::vector<PartitionOp> ops_;
   int next_op_ = 1;

@@ -94,6 +94,10 @@ WorkloadRequest workload_from_pod(const Json& pod, const std::string& gpu_resour
     }
   }
   if (spec.has("priority")) w.priority = spec.get("priority").as_int(w.priority);
+  if (w.expected_duration_s <= 0.0) {
+    w.expected_duration_s = std::atof(ann.get("kgwe.amd.com/expected-duration-seconds").str("0").c_str());
+    if (w.expected_duration_s <= 0.0) w.expected_duration_s = spec.get("activeDeadlineSeconds").as_number(0.0);
+  }
   for (const auto& kv : spec.get("nodeSelector").fields()) w.node_selector[kv.first] = kv.second.str();
   for (const auto& t : spec.get("tolerations").items()) {
     Toleration tl;
@@ -857,6 +861,9 @@ void Platform::refresh_gauges(double now_s) {
   }
   reg_->commit(std::move(batch));
   reg_->set("kgwe_workload_queue_depth", {}, static_cast<double>(queue_depth()));
+  const SchedulerMetrics sm = sched_->metrics();
+  reg_->set("kgwe_preemptions_deferred_total", {"wait"}, static_cast<double>(sm.preemptions_deferred_wait));
+  reg_->set("kgwe_preemptions_deferred_total", {"rate"}, static_cast<double>(sm.preemptions_rate_limited));
 }
 
 std::string Platform::expose_metrics() {

@@ -201,6 +201,7 @@ WorkloadRequest workload_from_json(const Json& in) {
   w.backend = backend_from(dc.get("backend").str("RCCL"));
   w.priority = spec.get("priority").as_int(0);
   w.preemptible = spec.get("preemptible").as_bool(true);
+  w.expected_duration_s = spec.get("expectedDurationSeconds").as_number(0.0);
   const Json& c = spec.has("constraints") ? spec.get("constraints") : spec;
   for (const auto& kv : c.get("nodeSelector").fields()) w.node_selector[kv.first] = kv.second.str();
   const Json& aff = c.get("affinity");
@@ -249,6 +250,7 @@ Json to_json(const WorkloadRequest& w) {
   j["world_size"] = w.world_size;
   j["priority"] = w.priority;
   j["preemptible"] = w.preemptible;
+  if (w.expected_duration_s > 0) j["expectedDurationSeconds"] = w.expected_duration_s;
   j["gang"] = w.gang;
   j["gang_size"] = w.gang_size;
   if (w.sharing != SharingMethod::None) {
@@ -293,6 +295,10 @@ Json to_json(const Decision& d) {
   return j;
 }
 
+static double wall_s() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
 Json to_json(const Allocation& a) {
   Json j = Json::object();
   j["uid"] = a.uid;
@@ -317,6 +323,11 @@ Json to_json(const Allocation& a) {
   j["type"] = to_string(a.type);
   j["priority"] = a.priority;
   j["preemptible"] = a.preemptible;
+  // Ledger times are on the monotonic clock; what leaves the process is wall
+  // time of the allocation and the expected run time (0 = unknown).
+  j["allocated_unix_s"] = a.allocated_ns ? wall_s() - static_cast<double>(now_ns() - a.allocated_ns) * 1e-9 : 0.0;
+  j["expected_duration_s"] =
+      a.expected_end_ns ? static_cast<double>(a.expected_end_ns - a.allocated_ns) * 1e-9 : 0.0;
   j["gang_pending"] = a.gang_pending;
   j["bandwidth_gbps"] = a.bandwidth_gbps;
   return j;
@@ -342,6 +353,12 @@ Allocation allocation_from_json(const Json& j) {
   a.type = workload_type_from(j.get("type").str("Training"));
   a.priority = j.get("priority").as_int(0);
   a.preemptible = j.get("preemptible").as_bool(true);
+  const double at = j.get("allocated_unix_s").as_number(0.0);
+  if (at > 0.0) {
+    a.allocated_ns = now_ns() - static_cast<int64_t>(std::max(0.0, wall_s() - at) * 1e9);
+    const double dur = j.get("expected_duration_s").as_number(0.0);
+    if (dur > 0.0) a.expected_end_ns = a.allocated_ns + static_cast<int64_t>(dur * 1e9);
+  }
   a.bandwidth_gbps = j.get("bandwidth_gbps").as_number(0.0);
   return a;
 }
@@ -463,6 +480,7 @@ std::vector<const PartitionInstance*> Scheduler::free_partitions(
     if (!w.arch.empty() && g.arch != w.arch) continue;
     if (gpu_owner_.count(g.uuid) || fenced_.count(g.uuid) || shared_.count(g.uuid))
       continue;  // whole GPU taken / shared / switching
+    if (!draining_gpus_.empty() && draining_gpus_.count(g.uuid)) continue;  // consolidation donor
     for (const auto& pi : g.partition.instances) {
       if (pi.in_use || part_owner_.count(pi.id)) continue;
       if (pi.memory_gb + 1e-9 < w.min_memory_gb) continue;
@@ -485,7 +503,9 @@ std::vector<std::string> Scheduler::cordoned() const {
   return {cordoned_.begin(), cordoned_.end()};
 }
 
-std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w) const {
+// The constraints that no release of capacity changes: cordon, selectors,
+// affinity, taints, placement relative to other workloads.
+std::string Scheduler::admissible(const NodeTopology& n, const WorkloadRequest& w) const {
   {
     std::lock_guard<std::mutex> lk(cordon_mu_);
     if (!cordoned_.empty() && cordoned_.count(n.name)) return "node cordoned (not ready)";
@@ -513,6 +533,12 @@ std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w)
     if (it != allocs_.end() && it->second.node != n.name)
       return "must co-locate with " + other + " on " + it->second.node;
   }
+  return "";
+}
+
+std::string Scheduler::eligible(const NodeTopology& n, const WorkloadRequest& w) const {
+  std::string why = admissible(n, w);
+  if (!why.empty()) return why;
   if (w.sharing != SharingMethod::None) {
     NodeScore tmp;
     if (!pick_share(n, w, &tmp))
@@ -968,6 +994,12 @@ bool Scheduler::share_fits(const GpuDevice& g, const WorkloadRequest& w, int* cu
   for (auto* c : clients) mem += c->share_memory_gb;
   const double cap = g.memory_total_gb > 0 ? g.memory_total_gb : 288.0;
   if (w.share_memory_gb > 0 && mem + w.share_memory_gb > cap + 1e-9) return false;
+  // HBM the device reports in use beyond what the ledger's clients were
+  // promised (another tenant, a leak) is not there for a new client either.
+  if (w.share_memory_gb > 0 && g.memory_total_gb > 0) {
+    const double unaccounted = std::max(0.0, g.memory_used_gb - mem);
+    if (mem + unaccounted + w.share_memory_gb > cap + 1e-9) return false;
+  }
   if (w.sharing == SharingMethod::TimeSlice) {
     if (static_cast<int>(clients.size()) >= cfg_.max_timeslice_replicas) return false;
     *cu_begin = 0;
@@ -1293,7 +1325,7 @@ Scheduler::NodeSummary Scheduler::node_summary(const NodeTopology& n) const {
       any_busy |= taken;
       free_n += taken ? 0 : 1;
     }
-    out.free_slices[p] = whole ? 0 : static_cast<uint8_t>(std::min(free_n, 255));
+    out.free_slices[p] = whole || draining_gpus_.count(g.uuid) ? 0 : static_cast<uint8_t>(std::min(free_n, 255));
     if (!any_busy && g.util.gfx_activity < 5.0 && p < 64) out.idle_mask |= 1ull << p;
   }
   std::lock_guard<std::mutex> ck(c.mu);
@@ -1330,30 +1362,14 @@ void Scheduler::filter_verdicts(const WorkloadRequest& w, const std::vector<std:
   // The ledger is read in chunks of kSweepChunk nodes: a sweep over 1,250
   // candidates must not hold binds / releases off the ledger for its whole
   // length (each node's verdict is advisory anyway: bind re-checks).
-  static const bool dbg = std::getenv("KGWE_SLOW_VERB_MS") != nullptr;
-  int64_t wait_ns = 0, t_l = dbg ? now_ns() : 0, worst_node_ns = 0;
   std::shared_lock<RwLock> lk(mu_);
-  if (dbg) wait_ns += now_ns() - t_l;
   auto mine = allocs_.find(w.uid);
   for (size_t i = 0; i < nodes.size(); ++i) {
     if ((i + 1) % kSweepChunk == 0) {
       lk.unlock();
-      if (dbg) t_l = now_ns();
       lk.lock();
-      if (dbg) wait_ns += now_ns() - t_l;
       mine = allocs_.find(w.uid);
     }
-    const int64_t t_n = dbg ? now_ns() : 0;
-    struct NodeTimer {
-      int64_t t0, *worst;
-      bool on;
-      ~NodeTimer() {
-        if (on) *worst = std::max(*worst, now_ns() - t0);
-      }
-    } nt{t_n, &worst_node_ns, dbg};
-    if (dbg && i + 1 == nodes.size() && wait_ns + worst_node_ns > 5000000)
-      std::fprintf(stderr, "kgwe filter_verdicts: lock wait %.2f ms, worst node %.2f ms\n", wait_ns / 1e6,
-                   worst_node_ns / 1e6);
     const std::string& name = nodes[i];
     auto it = snap->nodes.find(name);
     if (it == snap->nodes.end()) {
@@ -1406,6 +1422,19 @@ bool Scheduler::fence_gpu(const std::string& gpu_uuid, const std::string& node) 
   return true;
 }
 
+void Scheduler::set_draining(const std::string& gpu_uuid, const std::string& node, bool on) {
+  std::unique_lock<RwLock> lk(mu_);
+  const bool changed = on ? draining_gpus_.insert(gpu_uuid).second : draining_gpus_.erase(gpu_uuid) > 0;
+  if (!changed) return;
+  if (node.empty()) global_gen_.fetch_add(1);
+  else touch_node(node);
+}
+
+std::vector<std::string> Scheduler::draining() const {
+  std::shared_lock<RwLock> lk(mu_);
+  return {draining_gpus_.begin(), draining_gpus_.end()};
+}
+
 void Scheduler::unfence_gpu(const std::string& gpu_uuid, const std::string& node) {
   std::unique_lock<RwLock> lk(mu_);
   fenced_.erase(gpu_uuid);
@@ -1424,7 +1453,7 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
   for (const auto& p : s.partitions) {
     if (part_owner_.count(p)) return false;
     const std::string gpu = p.substr(0, p.rfind("/p"));
-    if (gpu_owner_.count(gpu) || fenced_.count(gpu) || shared_.count(gpu)) return false;
+    if (gpu_owner_.count(gpu) || fenced_.count(gpu) || shared_.count(gpu) || draining_gpus_.count(gpu)) return false;
   }
   if (w.sharing != SharingMethod::None) {
     // Re-check the CU range against the ledger as it is now (the score may
@@ -1451,9 +1480,11 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
     a.priority = w.priority;
     a.preemptible = w.preemptible;
     a.allocated_ns = now_ns();
+    a.expected_end_ns = expected_end_locked(w, a.allocated_ns);
     SharedGpu& sg = shared_[s.shared_gpu];
     sg.method = w.sharing;
     sg.clients.push_back(w.uid);
+    index_alloc_locked(a);
     allocs_[w.uid] = std::move(a);
     touch_node(s.node);
     return true;
@@ -1473,10 +1504,12 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
   a.preemptible = w.preemptible;
   a.gang_pending = gang_pending;
   a.allocated_ns = now_ns();
+  a.expected_end_ns = expected_end_locked(w, a.allocated_ns);
   a.bandwidth_gbps = s.bandwidth_gbps;
   for (const auto& g : s.gpus) gpu_owner_[g] = w.uid;
   for (const auto& p : s.partitions) part_owner_[p] = w.uid;
   node_gpus_used_[s.node] += static_cast<int>(s.gpus.size());
+  index_alloc_locked(a);
   allocs_[w.uid] = std::move(a);
   touch_node(s.node);
   return true;
@@ -1497,7 +1530,30 @@ void Scheduler::erase_locked(std::unordered_map<std::string, Allocation>::iterat
       if (cl.empty()) shared_.erase(sh);
     }
   }
+  auto na = node_allocs_.find(a.node);
+  if (na != node_allocs_.end()) {
+    auto& v = na->second;
+    auto pos = std::find(v.begin(), v.end(), a.uid);
+    if (pos != v.end()) {
+      *pos = std::move(v.back());
+      v.pop_back();
+    }
+    if (v.empty()) node_allocs_.erase(na);
+  }
   allocs_.erase(it);
+}
+
+void Scheduler::index_alloc_locked(const Allocation& a) { node_allocs_[a.node].push_back(a.uid); }
+
+// Caller holds mu_.  When the workload says how long it runs, that; else the
+// learned mean lifetime of its type once 8 allocations of it have completed.
+int64_t Scheduler::expected_end_locked(const WorkloadRequest& w, int64_t start_ns) const {
+  double s = w.expected_duration_s;
+  if (s <= 0.0) {
+    const Lifetime& l = lifetimes_[static_cast<int>(w.type) & 7];
+    if (l.n >= 8) s = l.mean_s;
+  }
+  return s > 0.0 ? start_ns + static_cast<int64_t>(s * 1e9) : 0;
 }
 
 void Scheduler::emit(SchedEvent e) {
@@ -1545,8 +1601,13 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
     latency_.record_ms(dd.latency_ms);
     std::lock_guard<std::mutex> lk(stat_mu_);
     stats_.attempts++;
-    if (dd.ok) stats_.scheduled++;
-    else stats_.failed++;
+    if (dd.ok) {
+      stats_.scheduled++;
+      note_placement();
+      preempt_wait_.erase(dd.uid);
+    } else {
+      stats_.failed++;
+    }
   };
   {
     std::shared_lock<RwLock> lk(mu_);
@@ -1623,10 +1684,7 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
       finish(d);
       return d;
     }
-    if (attempt == 0 && cfg_.enable_preemption && w.priority > 0) {
-      std::unique_lock<RwLock> lk(mu_);
-      if (try_preempt(w, snap, &d)) continue;
-    }
+    if (attempt == 0 && cfg_.enable_preemption && w.priority > 0 && try_preempt(w, snap, &d)) continue;
     break;
   }
   d.ok = false;
@@ -1636,15 +1694,79 @@ Decision Scheduler::schedule(const WorkloadRequest& w) {
   return d;
 }
 
-// Caller holds mu_ exclusively.  Picks, over all nodes, the cheapest set of
-// lower-priority preemptible allocations whose removal makes the node
-// eligible; cost = (sum of victim priorities, #victims, victim GPUs).
-// Caller holds mu_ exclusively (the ledger is temporarily edited and
-// restored).  The cheapest set of lower-priority preemptible allocations
-// (whole gangs) whose removal makes node `n` eligible for `w`; false if none.
-bool Scheduler::plan_node_preemption(const WorkloadRequest& w, const NodeTopology& n,
-                                     std::vector<std::string>* victims_out,
-                                     std::tuple<int64_t, size_t, size_t>* cost_out) {
+// An allocation expected to finish before `soon_ns`, and not overdue by more
+// than its own expected run time (an estimate that far off says nothing).
+bool Scheduler::near_completion(const Allocation& a, int64_t now, int64_t soon_ns) const {
+  if (!a.expected_end_ns || a.expected_end_ns > soon_ns) return false;
+  return now - a.expected_end_ns <= a.expected_end_ns - a.allocated_ns;
+}
+
+// Caller holds mu_ (shared).  Walks only the allocations on `n`.  Room is
+// counted in GPUs (a slice = 1/8, a share = 1/8: generous, so "false" is a
+// true negative); the cost is that of the cheapest victims, in eviction
+// order, whose room covers the shortfall.
+bool Scheduler::estimate_node_preemption(const WorkloadRequest& w, const NodeTopology& n, int64_t now,
+                                         int64_t soon_ns, PreemptCost* cost, bool* wait) const {
+  *wait = false;
+  auto na = node_allocs_.find(n.name);
+  if (na == node_allocs_.end()) return false;
+  const bool frac = w.partition || w.sharing != SharingMethod::None;
+  const double need = frac ? std::max(1, w.partition ? w.partition_count : 1) / 8.0 : std::max(1, w.gpu_count);
+  auto room_of = [&](const Allocation& a) {
+    const double whole = static_cast<double>(a.gpus.size());
+    const double part = (a.partitions.size() + (a.shared_gpu.empty() ? 0 : 1)) / 8.0;
+    return frac ? whole + part : whole + part;  // slices free a whole GPU only together: still an upper bound
+  };
+  struct Cand {
+    int64_t prio, age_ns;
+    double room;
+  };
+  std::vector<Cand> cands;
+  double held = 0.0, soon = 0.0;
+  for (const auto& uid : na->second) {
+    auto it = allocs_.find(uid);
+    if (it == allocs_.end()) continue;
+    const Allocation& a = it->second;
+    const double r = room_of(a);
+    held += r;
+    if (near_completion(a, now, soon_ns)) {
+      soon += r;
+      continue;  // about to finish: not a victim
+    }
+    if (a.preemptible && a.priority < w.priority) cands.push_back({a.priority, a.allocated_ns, r});
+  }
+  const double free_now = std::max(0.0, static_cast<double>(n.gpus.size()) - held);
+  if (soon > 0.0 && free_now + soon >= need) *wait = true;
+  if (cands.empty()) return false;
+  std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+    return a.prio != b.prio ? a.prio < b.prio : a.age_ns > b.age_ns;
+  });
+  double room = free_now;
+  int64_t prio = 0;
+  size_t k = 0;
+  for (const auto& c : cands) {
+    room += c.room;
+    prio += c.prio;
+    ++k;
+    if (room >= need) break;
+  }
+  if (room < need && !frac) return false;
+  *cost = {prio, k, static_cast<size_t>(room * 8)};
+  return true;
+}
+
+// Caller holds mu_ exclusively (the ledger is edited and restored).  The
+// cheapest set of lower-priority preemptible allocations (whole gangs) on
+// `n`, none expected to finish before `protect_until_ns`, whose removal makes
+// the node eligible for `w`; false if there is none.
+bool Scheduler::plan_node_preemption(const WorkloadRequest& w, const NodeTopology& n, int64_t protect_until_ns,
+                                     std::vector<std::string>* victims_out, PreemptCost* cost_out) {
+  auto na = node_allocs_.find(n.name);
+  if (na == node_allocs_.end()) return false;
+  const int64_t now = now_ns();
+  auto victim_ok = [&](const Allocation& a) {
+    return a.preemptible && a.priority < w.priority && !near_completion(a, now, protect_until_ns);
+  };
   // A gang is preempted as a unit: its other members (on any node) would
   // otherwise keep their GPUs while the job cannot run.
   auto unit_of = [&](const Allocation& a, std::vector<const Allocation*>* out) {
@@ -1652,17 +1774,24 @@ bool Scheduler::plan_node_preemption(const WorkloadRequest& w, const NodeTopolog
       out->push_back(&a);
       return true;
     }
-    for (const auto& kv : allocs_)
-      if (kv.second.gang == a.gang) {
-        if (!kv.second.preemptible || kv.second.priority >= w.priority) return false;
-        out->push_back(&kv.second);
-      }
+    auto g = gangs_.find(a.gang);
+    if (g == gangs_.end()) {
+      out->push_back(&a);
+      return true;
+    }
+    for (const auto& m : g->second.members) {
+      auto it = allocs_.find(m);
+      if (it == allocs_.end()) continue;
+      if (!victim_ok(it->second)) return false;
+      out->push_back(&it->second);
+    }
     return true;
   };
   std::vector<const Allocation*> cands;
-  for (const auto& a : allocs_)
-    if (a.second.node == n.name && a.second.preemptible && a.second.priority < w.priority)
-      cands.push_back(&a.second);
+  for (const auto& uid : na->second) {
+    auto it = allocs_.find(uid);
+    if (it != allocs_.end() && victim_ok(it->second)) cands.push_back(&it->second);
+  }
   if (cands.empty()) return false;
   std::sort(cands.begin(), cands.end(), [](const Allocation* a, const Allocation* b) {
     if (a->priority != b->priority) return a->priority < b->priority;
@@ -1719,41 +1848,150 @@ bool Scheduler::plan_node_preemption(const WorkloadRequest& w, const NodeTopolog
   return true;
 }
 
-// Caller holds mu_ exclusively.  Picks, over all nodes, the cheapest victim
-// set; cost = (sum of victim priorities, #victims, victim GPUs).
-bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d) {
-  std::string best_node;
-  std::vector<std::string> best;
-  std::tuple<int64_t, size_t, size_t> best_cost{INT64_MAX, 0, 0};
-  for (const auto& kv : snap->nodes) {
-    std::vector<std::string> victims;
-    std::tuple<int64_t, size_t, size_t> cost;
-    if (!plan_node_preemption(w, kv.second, &victims, &cost)) continue;
-    if (cost < best_cost) {
-      best_node = kv.first;
-      best = std::move(victims);
-      best_cost = cost;
+// Caller holds stat_mu_.  Victims the rate window still allows: a percentage
+// of the placements inside the window, never less than the burst.
+int Scheduler::preemption_budget_locked(int64_t now) {
+  if (cfg_.preemption_max_rate_percent <= 0.0) return INT32_MAX;
+  const int64_t sec = now / 1000000000;
+  while (!rate_.empty() && rate_.front().sec <= sec - std::max(1, cfg_.preemption_window_s)) rate_.pop_front();
+  uint64_t placed = 0, victims = 0;
+  for (const auto& b : rate_) {
+    placed += b.placed;
+    victims += b.victims;
+  }
+  const double allowed =
+      std::max<double>(cfg_.preemption_burst, cfg_.preemption_max_rate_percent * 0.01 * static_cast<double>(placed));
+  return static_cast<int>(std::max(0.0, std::floor(allowed) - static_cast<double>(victims)));
+}
+
+void Scheduler::note_placement() {  // caller holds stat_mu_
+  const int64_t sec = now_ns() / 1000000000;
+  if (rate_.empty() || rate_.back().sec != sec) rate_.push_back({sec, 0, 0});
+  rate_.back().placed++;
+}
+
+std::vector<Scheduler::PreemptPlan> Scheduler::select_preemption(const WorkloadRequest& w,
+                                                                 const TopologySnapshot& snap,
+                                                                 const std::vector<std::string>* nodes,
+                                                                 bool commit) {
+  std::vector<PreemptPlan> out;
+  const int64_t now = now_ns();
+  // ---- policy: window budget, and whether this request may still be told to wait
+  int budget;
+  bool may_wait = cfg_.preemption_wait_window_s > 0.0 && w.priority < cfg_.preemption_urgent_priority;
+  {
+    std::lock_guard<std::mutex> sl(stat_mu_);
+    budget = preemption_budget_locked(now);
+    if (budget <= 0) {
+      stats_.preemptions_rate_limited++;
+      return out;
+    }
+    if (may_wait) {
+      auto it = preempt_wait_.find(w.uid);
+      if (it != preempt_wait_.end() &&
+          now - it->second > static_cast<int64_t>(cfg_.preemption_max_wait_s * 1e9))
+        may_wait = false;  // waited long enough: completions did not make room
     }
   }
-  if (best_node.empty()) return false;
-  for (const auto& uid : best) {
-    auto it = allocs_.find(uid);
-    if (it == allocs_.end()) continue;
-    const std::string gang = it->second.gang;
-    const std::string node = it->second.node;
-    erase_locked(it);
-    if (!gang.empty()) {
-      auto g = gangs_.find(gang);
-      if (g != gangs_.end()) {
-        g->second.members.erase(uid);
-        if (g->second.members.empty()) gangs_.erase(g);
+  const int64_t soon = now + static_cast<int64_t>(cfg_.preemption_wait_window_s * 1e9);
+  const int64_t protect = may_wait ? soon : 0;  // past its patience a request may also evict near-finishers
+
+  // ---- estimates over the candidates, under the shared lock
+  struct Est {
+    const NodeTopology* n;
+    PreemptCost cost;
+  };
+  std::vector<Est> est;
+  bool wait_node = false;
+  {
+    std::shared_lock<RwLock> lk(mu_);
+    auto visit = [&](const NodeTopology& n) {
+      PreemptCost c;
+      bool wait = false;
+      const bool ok = estimate_node_preemption(w, n, now, protect, &c, &wait);
+      // waiting only helps on a node the request could run on at all
+      if (wait && !wait_node) wait_node = admissible(n, w).empty();
+      if (ok) est.push_back({&n, c});
+    };
+    if (nodes) {
+      for (const auto& name : *nodes) {
+        auto it = snap->nodes.find(name);
+        if (it != snap->nodes.end()) visit(it->second);
+      }
+    } else {
+      for (const auto& kv : snap->nodes) visit(kv.second);
+    }
+  }
+  if (may_wait && wait_node) {
+    std::lock_guard<std::mutex> sl(stat_mu_);
+    stats_.preemptions_deferred_wait++;
+    preempt_wait_.emplace(w.uid, now);
+    if (preempt_wait_.size() > 65536) {  // requests that went away without ever being placed
+      for (auto it = preempt_wait_.begin(); it != preempt_wait_.end();)
+        it = now - it->second > 3600LL * 1000000000 ? preempt_wait_.erase(it) : std::next(it);
+    }
+    return out;
+  }
+  if (est.empty()) return out;
+  auto cheaper = [](const Est& a, const Est& b) {
+    return a.cost != b.cost ? a.cost < b.cost : a.n->name < b.n->name;
+  };
+  const size_t K = static_cast<size_t>(std::max(1, cfg_.preemption_candidate_nodes));
+
+  // ---- exact plans on the K cheapest (then the next K, at most 4 rounds), under the exclusive lock
+  size_t done = 0;
+  for (int round = 0; round < 4 && done < est.size() && out.empty(); ++round) {
+    const size_t end = std::min(est.size(), done + K);
+    std::partial_sort(est.begin() + done, est.begin() + end, est.end(), cheaper);
+    std::unique_lock<RwLock> lk(mu_);
+    for (size_t i = done; i < end; ++i) {
+      PreemptPlan p;
+      p.node = est[i].n->name;
+      if (!plan_node_preemption(w, *est[i].n, protect, &p.victims, &p.cost)) continue;
+      // over the window's budget: only the window's first preemption may exceed it
+      if (static_cast<int>(p.victims.size()) > budget && budget < cfg_.preemption_burst) continue;
+      out.push_back(std::move(p));
+    }
+    done = end;
+    if (out.empty()) continue;
+    std::sort(out.begin(), out.end(), [](const PreemptPlan& a, const PreemptPlan& b) {
+      return a.cost != b.cost ? a.cost < b.cost : a.node < b.node;
+    });
+    if (commit) {
+      out.resize(1);
+      for (const auto& uid : out[0].victims) {
+        auto it = allocs_.find(uid);
+        if (it == allocs_.end()) continue;
+        const std::string gang = it->second.gang;
+        const std::string node = it->second.node;
+        erase_locked(it);
+        if (!gang.empty()) {
+          auto g = gangs_.find(gang);
+          if (g != gangs_.end()) {
+            g->second.members.erase(uid);
+            if (g->second.members.empty()) gangs_.erase(g);
+          }
+        }
+        emit({SchedEventType::Preempted, uid, node, "by " + w.uid, now_ns()});
       }
     }
-    d->preempted.push_back(uid);
-    emit({SchedEventType::Preempted, uid, node, "by " + w.uid, now_ns()});
   }
-  std::lock_guard<std::mutex> sl(stat_mu_);
-  stats_.preemptions += best.size();
+  if (!out.empty()) {  // book the cheapest plan's victims in the window
+    std::lock_guard<std::mutex> sl(stat_mu_);
+    const int64_t sec = now / 1000000000;
+    if (rate_.empty() || rate_.back().sec != sec) rate_.push_back({sec, 0, 0});
+    rate_.back().victims += static_cast<uint32_t>(out[0].victims.size());
+    if (commit) stats_.preemptions += out[0].victims.size();
+  }
+  return out;
+}
+
+// Picks, over all nodes, the cheapest victim set and evicts it from the
+// ledger; cost = (sum of victim priorities, #victims, victim GPUs).
+bool Scheduler::try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d) {
+  auto plans = select_preemption(w, snap, nullptr, /*commit=*/true);
+  if (plans.empty()) return false;
+  for (const auto& uid : plans[0].victims) d->preempted.push_back(uid);
   return true;
 }
 
@@ -1762,18 +2000,17 @@ std::map<std::string, std::vector<std::string>> Scheduler::preemption_plans(
   std::map<std::string, std::vector<std::string>> out;
   if (!cfg_.enable_preemption || w.priority <= 0) return out;
   auto snap = disc_->snapshot();
-  std::unique_lock<RwLock> lk(mu_);  // plans edit (and restore) the ledger
-  for (const auto& name : nodes) {
-    auto it = snap->nodes.find(name);
-    if (it == snap->nodes.end()) continue;
-    if (eligible(it->second, w).empty()) {
-      out[name] = {};  // fits without victims
-      continue;
+  {  // a candidate that fits as it is needs no victims
+    std::shared_lock<RwLock> lk(mu_);
+    const uint64_t sig = request_signature(w);
+    std::string scratch;
+    for (const auto& name : nodes) {
+      auto it = snap->nodes.find(name);
+      if (it != snap->nodes.end() && eligible_cached(it->second, w, sig, &scratch).empty()) out[name] = {};
     }
-    std::vector<std::string> victims;
-    std::tuple<int64_t, size_t, size_t> cost;
-    if (plan_node_preemption(w, it->second, &victims, &cost)) out[name] = std::move(victims);
   }
+  if (!out.empty()) return out;
+  for (auto& p : select_preemption(w, snap, &nodes, /*commit=*/false)) out[p.node] = std::move(p.victims);
   return out;
 }
 
@@ -1905,13 +2142,27 @@ std::vector<Decision> Scheduler::schedule_gang(const std::vector<WorkloadRequest
       d.shared_gpu.clear();
     }
   }
+  if (ok) {  // the gang is complete from the start: its members are found (and preempted) as one unit
+    for (const auto& w : members) {
+      if (w.gang.empty()) continue;
+      Gang& gg = gangs_[w.gang];
+      gg.size = std::max<int>(gg.size, std::max<int>(w.gang_size, static_cast<int>(members.size())));
+      if (gg.members.empty()) gg.first_ns = now_ns();
+      gg.members.insert(w.uid);
+      gg.ready = true;
+    }
+  }
   lk.unlock();
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   latency_.record_ms(ms);
   std::lock_guard<std::mutex> sl(stat_mu_);
   stats_.attempts += members.size();
-  if (ok) stats_.scheduled += members.size();
-  else stats_.failed += members.size();
+  if (ok) {
+    stats_.scheduled += members.size();
+    for (size_t i = 0; i < members.size(); ++i) note_placement();
+  } else {
+    stats_.failed += members.size();
+  }
   return out;
 }
 
@@ -2009,6 +2260,8 @@ Decision Scheduler::bind(const WorkloadRequest& w, const std::string& node) {
   std::lock_guard<std::mutex> sl(stat_mu_);
   stats_.attempts++;
   stats_.scheduled++;
+  note_placement();
+  preempt_wait_.erase(w.uid);
   if (optimal) stats_.topology_optimal++;
   return d;
 }
@@ -2065,6 +2318,12 @@ bool Scheduler::release(const std::string& uid) {
         if (g->second.members.empty()) gangs_.erase(g);
       }
     }
+    if (!it->second.gang_pending && it->second.allocated_ns) {  // a completed run: learn its lifetime
+      Lifetime& l = lifetimes_[static_cast<int>(it->second.type) & 7];
+      const double s = static_cast<double>(now_ns() - it->second.allocated_ns) * 1e-9;
+      l.n++;
+      l.mean_s += (s - l.mean_s) / static_cast<double>(std::min<uint64_t>(l.n, 64));
+    }
     erase_locked(it);
   }
   emit({SchedEventType::Released, uid, node, "", now_ns()});
@@ -2103,6 +2362,7 @@ bool Scheduler::restore(const Allocation& a) {
     if (!gg.first_ns) gg.first_ns = c.allocated_ns;
     c.gang_pending = false;
   }
+  index_alloc_locked(c);
   allocs_[a.uid] = c;
   touch_node(a.node);
   return true;
@@ -2118,7 +2378,7 @@ bool Scheduler::migrate_partition(const std::string& uid, const std::string& fro
     auto pos = std::find(parts.begin(), parts.end(), from);
     if (pos == parts.end() || part_owner_.count(to)) return false;
     const std::string gpu = to.substr(0, to.rfind("/p"));
-    if (gpu_owner_.count(gpu) || fenced_.count(gpu) || shared_.count(gpu)) return false;
+    if (gpu_owner_.count(gpu) || fenced_.count(gpu) || shared_.count(gpu) || draining_gpus_.count(gpu)) return false;
     auto snap = disc_->snapshot();
     std::string to_node;
     for (const auto& kv : snap->nodes)

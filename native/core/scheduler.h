@@ -113,6 +113,11 @@ struct WorkloadRequest {
   double share_memory_gb = 0.0;    // 0 = no cap
   double max_latency_ms = 0.0;
   std::vector<std::string> preferred_nodes;  // optimizer hint (+10 bonus)
+  // How long the workload is expected to hold its GPUs (spec
+  // expectedDurationSeconds, pod annotation kgwe.amd.com/expected-duration-seconds
+  // or spec.activeDeadlineSeconds); 0 = unknown (the scheduler's learned
+  // per-type mean is used once it has enough samples).
+  double expected_duration_s = 0.0;
 };
 
 WorkloadRequest workload_from_json(const Json& j);
@@ -144,6 +149,7 @@ struct Allocation {
   bool preemptible = true;
   bool gang_pending = false;  // reserved, waiting for the rest of its gang
   int64_t allocated_ns = 0;
+  int64_t expected_end_ns = 0;  // 0 = unknown
   double bandwidth_gbps = 0.0;
 };
 
@@ -184,6 +190,19 @@ struct SchedulerConfig {
   int max_share_clients = 8;          // co-located clients per GPU
   double default_cu_percent = 12.5;   // one XCD (32 of 256 CUs)
   int max_timeslice_replicas = 4;
+  // Preemption policy.  Victims are planned exactly only on the K nodes a
+  // cheap per-node estimate ranks best; an allocation expected to finish
+  // within the wait window is not a victim, and a request whose room such
+  // allocations will free waits for them instead (up to max wait; requests at
+  // or above the urgent priority never wait); victims per sliding window are
+  // capped at a percentage of the placements in it (plus a small burst).
+  int preemption_candidate_nodes = 8;
+  double preemption_wait_window_s = 30.0;   // 0 = never prefer waiting
+  double preemption_max_wait_s = 120.0;
+  int64_t preemption_urgent_priority = 1000000;
+  double preemption_max_rate_percent = 4.0;  // 0 = no cap
+  int preemption_window_s = 300;
+  int preemption_burst = 8;
 };
 
 enum class SchedEventType { Scheduled, Failed, Released, Preempted, GangReady, GangTimeout, Migrated };
@@ -196,7 +215,9 @@ const char* to_string(SchedEventType t);
 
 struct SchedulerMetrics {
   uint64_t attempts = 0, scheduled = 0, failed = 0, topology_optimal = 0, preemptions = 0,
-           releases = 0, gang_timeouts = 0;
+           releases = 0, gang_timeouts = 0,
+           preemptions_deferred_wait = 0,   // requests told to wait for a near completion
+           preemptions_rate_limited = 0;    // requests refused by the window cap
   double avg_latency_ms = 0.0, p50_ms = 0.0, p90_ms = 0.0, p99_ms = 0.0, max_ms = 0.0;
   size_t active_allocations = 0, allocated_gpus = 0, allocated_partitions = 0, shared_gpus = 0,
          share_clients = 0;
@@ -225,11 +246,14 @@ class Scheduler {
                          std::vector<int>* totals);
   // Reserve on a given node (bind verb); honours gangs (may return Waiting).
   Decision bind(const WorkloadRequest& w, const std::string& node);
-  // Extender preempt verb: per candidate node, the cheapest victim set that
-  // makes room for `w` (empty = fits as is; absent = impossible).  Dry run.
+  // Extender preempt verb: for the best candidate nodes (at most
+  // preemption_candidate_nodes of them), the cheapest victim set that makes
+  // room for `w` (empty = fits as is; absent = impossible, or preemption is
+  // deferred by the wait / rate policy).  Dry run; the cheapest returned plan
+  // is charged to the rate window.
   std::map<std::string, std::vector<std::string>> preemption_plans(const WorkloadRequest& w,
                                                                    const std::vector<std::string>& nodes);
-  void count_preemptions(size_t n);
+  void count_preemptions(size_t n);  // victims evicted by kube-scheduler after a dry-run plan (statistics)
   // Permit-stage check for a gang member: "Allow" | "Wait" | "Reject".
   std::string permit(const std::string& uid);
 
@@ -266,6 +290,11 @@ class Scheduler {
   // snapshot could otherwise reserve the GPU (or a slice of it).
   bool fence_gpu(const std::string& gpu_uuid, const std::string& node = "");
   void unfence_gpu(const std::string& gpu_uuid, const std::string& node = "");
+  // Consolidation donor: no NEW slice reservations on the GPU (existing ones
+  // stay until their pods are evicted); whole-GPU requests never land on a
+  // partitioned GPU anyway.
+  void set_draining(const std::string& gpu_uuid, const std::string& node, bool on);
+  std::vector<std::string> draining() const;
   // Cordon: no new placements on the node (NotReady / draining); existing
   // allocations are untouched.
   void set_cordon(const std::string& node, bool on);
@@ -283,6 +312,7 @@ class Scheduler {
   // Exposed for tests / the optimizer: score one node for a request.
   NodeScore score_node(const NodeTopology& n, const WorkloadRequest& w) const;
   std::string eligible(const NodeTopology& n, const WorkloadRequest& w) const;  // "" = ok
+  std::string admissible(const NodeTopology& n, const WorkloadRequest& w) const;  // eligible() minus capacity
 
  private:
   struct Ctx;  // per-call view of the ledger for one node
@@ -304,9 +334,31 @@ class Scheduler {
   bool share_fits(const GpuDevice& g, const WorkloadRequest& w, int* cu_begin, int* cu_end) const;
   bool reserve_locked(const WorkloadRequest& w, const NodeScore& s, bool gang_pending);
   void erase_locked(std::unordered_map<std::string, Allocation>::iterator it);
+  using PreemptCost = std::tuple<int64_t, size_t, size_t>;  // (sum of victim priorities, victims, GPUs)
+  struct PreemptPlan {
+    std::string node;
+    std::vector<std::string> victims;
+    PreemptCost cost{0, 0, 0};
+  };
   bool try_preempt(const WorkloadRequest& w, const TopologySnapshot& snap, Decision* d);
-  bool plan_node_preemption(const WorkloadRequest& w, const NodeTopology& n, std::vector<std::string>* victims,
-                            std::tuple<int64_t, size_t, size_t>* cost);
+  // Exact plans on the best candidate nodes (see SchedulerConfig).  With
+  // `commit` the cheapest plan's victims are erased under the same exclusive
+  // lock hold that validated it, and only that plan is returned.
+  std::vector<PreemptPlan> select_preemption(const WorkloadRequest& w, const TopologySnapshot& snap,
+                                             const std::vector<std::string>* nodes, bool commit);
+  bool plan_node_preemption(const WorkloadRequest& w, const NodeTopology& n, int64_t protect_until_ns,
+                            std::vector<std::string>* victims, PreemptCost* cost);
+  // Shared lock.  Cheap upper-bound estimate for one node: false if even
+  // evicting every eligible victim cannot make room; *wait = the room will be
+  // freed by allocations expected to finish before `soon_ns`.
+  bool estimate_node_preemption(const WorkloadRequest& w, const NodeTopology& n, int64_t now, int64_t soon_ns,
+                                PreemptCost* cost, bool* wait) const;
+  bool near_completion(const Allocation& a, int64_t now, int64_t soon_ns) const;
+  void index_alloc_locked(const Allocation& a);
+  int64_t expected_end_locked(const WorkloadRequest& w, int64_t start_ns) const;
+  // Rate window (stat_mu_): victims still allowed now; charge() books them.
+  int preemption_budget_locked(int64_t now);
+  void note_placement();
   void emit(SchedEvent e);
   double bandwidth_of(const NodeTopology& n, const std::vector<std::string>& gpus) const;
 
@@ -323,10 +375,19 @@ class Scheduler {
   };
   std::unordered_map<std::string, SharedGpu> shared_;        // gpu uuid -> clients
   std::set<std::string> fenced_;                             // GPUs mid partition switch
+  std::set<std::string> draining_gpus_;                      // consolidation donors: no new slices
   mutable std::mutex cordon_mu_;
   std::set<std::string> cordoned_;
   bool gpu_has_slice_owner_locked(const std::string& gpu_uuid) const;
   std::unordered_map<std::string, int> node_gpus_used_;      // node -> allocated GPUs
+  std::unordered_map<std::string, std::vector<std::string>> node_allocs_;  // node -> uids on it
+  // Learned mean lifetime per workload type (released allocations only), for
+  // allocations that do not say how long they expect to run.
+  struct Lifetime {
+    double mean_s = 0.0;
+    uint64_t n = 0;
+  };
+  Lifetime lifetimes_[8];
   struct Gang {
     int size = 0;
     std::set<std::string> members;
@@ -373,6 +434,12 @@ class Scheduler {
 
   mutable std::mutex stat_mu_;
   SchedulerMetrics stats_;
+  struct RateBucket {
+    int64_t sec = 0;
+    uint32_t placed = 0, victims = 0;
+  };
+  std::deque<RateBucket> rate_;                              // one bucket per second with activity
+  std::unordered_map<std::string, int64_t> preempt_wait_;    // uid -> first time it was told to wait
   LatencyHistogram latency_;
 
   mutable std::mutex ev_mu_;

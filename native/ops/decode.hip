@@ -316,7 +316,8 @@ namespace {
 int decode_attn_impl(const void* q, void* kcache, void* vcache, const float* cos_t, const float* sin_t,
                      const int* lens, float* workspace, void* out, int B, int Hq, int Hkv, int D, int Smax,
                      int splits, float scale, hipStream_t st) {
-  if (B <= 0 || Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || Smax <= 0) return -1;
+  // The merge step reads one split's partial per lane of a 64-wide wave.
+  if (B <= 0 || Hkv <= 0 || Hq % Hkv != 0 || splits <= 0 || splits > 64 || Smax <= 0) return -1;
   const int G = Hq / Hkv;
   float* po = workspace;
   float* pml = workspace + static_cast<int64_t>(B) * Hq * splits * D;

@@ -192,8 +192,21 @@ def test_controller_actuates_pushed_node_partitions_through_the_agent(tmp_path):
     try:
         body = dict(agent.topology)
         body["agent_endpoint"] = f"127.0.0.1:{agent.grpc_port}"
-        req = urllib.request.Request(f"{ext.url}/v1/nodes/edge/topology", data=json.dumps(body).encode(),
-                                     headers={"Content-Type": "application/json"})
+        url = f"{ext.url}/v1/nodes/edge/topology"
+        # a push without the token is refused outright: it could redirect the token-bearing
+        # SetPartition call to an endpoint of its choosing
+        rogue = dict(body, agent_endpoint="203.0.113.9:50052")
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(urllib.request.Request(
+                url, data=json.dumps(rogue).encode(), headers={"Content-Type": "application/json"}), timeout=5)
+        assert ei.value.code == 401
+        with pytest.raises(urllib.error.HTTPError):
+            urllib.request.urlopen(urllib.request.Request(
+                url, data=json.dumps(rogue).encode(),
+                headers={"Content-Type": "application/json", "Authorization": "Bearer wrong"}), timeout=5)
+        assert plat.node("edge") is None
+        req = urllib.request.Request(url, data=json.dumps(body).encode(),
+                                     headers={"Content-Type": "application/json", "Authorization": "Bearer tkn"})
         assert urllib.request.urlopen(req, timeout=5).status == 200
         d = plat.schedule({"uid": "slice", "workloadType": "Inference",
                            "gpuRequirements": {"count": 0, "partition": {"mode": "CPX", "count": 1}}})
@@ -205,3 +218,45 @@ def test_controller_actuates_pushed_node_partitions_through_the_agent(tmp_path):
     finally:
         ext.stop()
         gsrv.stop(0)
+
+
+def test_advertised_endpoint_must_be_an_address_of_the_node_object(tmp_path):
+    """With an apiserver the controller pins an agent's endpoint to the Node
+    object's own addresses: an authenticated push naming another host keeps
+    its topology but not its endpoint."""
+    import urllib.request
+
+    from kgwe.controller.apiserver import FakeApiServer
+    from kgwe.controller.kube import KubeClient
+    from kgwe.controller.main import DEFAULTS as CDEF
+    from kgwe.controller.main import build
+
+    tok = tmp_path / "token"
+    tok.write_text("tkn")
+    api = FakeApiServer().start()
+    try:
+        KubeClient(api.url).create_node({
+            "apiVersion": "v1", "kind": "Node", "metadata": {"name": "edge"},
+            "status": {"addresses": [{"type": "InternalIP", "address": "10.0.0.5"},
+                                     {"type": "Hostname", "address": "edge"}]}})
+        ccfg = load_config(CDEF, sets=["listen.host=127.0.0.1", "listen.port=0", f"kube.url={api.url}",
+                                       f"agentActuation.tokenFile={tok}", "labelNodes=false"])
+        plat, ext, _ = build(ccfg)
+        ext.start()
+        try:
+            def push(endpoint):
+                body = dict(make_fixture("edge", 8, 2), agent_endpoint=endpoint)
+                req = urllib.request.Request(
+                    f"{ext.url}/v1/nodes/edge/topology", data=json.dumps(body).encode(),
+                    headers={"Content-Type": "application/json", "Authorization": "Bearer tkn"})
+                return json.loads(urllib.request.urlopen(req, timeout=5).read())
+
+            r = push("203.0.113.9:50052")
+            assert r["ok"] and "not an address of Node edge" in r["endpointIgnored"]
+            assert plat.node("edge") is not None
+            assert push("10.0.0.5:50052") == {"ok": True}
+            assert push("edge:50052") == {"ok": True}
+        finally:
+            ext.stop()
+    finally:
+        api.stop()

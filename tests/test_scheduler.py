@@ -306,3 +306,101 @@ def test_scale_bench_small_fleet():
     r = scale.run(nodes=128, ops=600, live_max=300)
     assert r["scheduled"] > 500
     assert r["schedule_ms"]["p99"] < 40.0 and r["topology_query_ms"]["p99"] < 40.0
+
+
+# --- preemption policy: K best nodes, prefer waiting, rate window -----------------------------
+
+def _alloc(p, uid):
+    return next((a for a in p.allocations() if a["uid"] == uid), None)
+
+
+def _full_fleet(p, nodes, priority=10, **spec):
+    for i in range(nodes):
+        p.add_fake_node(make_fixture(f"f{i:03d}", 8, 2))
+    for i in range(nodes):
+        assert p.schedule(wl(f"low{i:03d}", 8, priority=priority, **spec))["ok"]
+
+
+def test_preemption_plans_exactly_on_the_cheapest_nodes_of_a_large_fleet():
+    p = Platform({"scheduler": {"preemptionCandidateNodes": 4, "preemptionWaitWindowSeconds": 0}})
+    for i in range(40):
+        p.add_fake_node(make_fixture(f"f{i:03d}", 8, 2))
+    # every node full; node f017 holds the only priority-1 job, f005 only non-preemptible work
+    for i in range(40):
+        sel = {"nodeSelector": {"kubernetes.io/hostname": f"f{i:03d}"}}
+        pr, pre = (1, True) if i == 17 else (50, False) if i == 5 else (20, True)
+        assert p.schedule(wl(f"j{i:03d}", 8, priority=pr, preemptible=pre, constraints=sel))["ok"]
+    d = p.schedule(wl("vip", 8, priority=100))
+    assert d["ok"] and d["preempted"] == ["j017"] and d["node"] == "f017"
+    # the extender's dry run: at most K candidate plans, the non-preemptible node never among them
+    plans = json.loads(p.preempt(json.dumps({
+        "pod": {"metadata": {"name": "vip2", "uid": "vip2"},
+                "spec": {"priority": 100, "containers": [{"resources": {"limits": {"amd.com/gpu": "8"}}}]}},
+        "nodeNameToMetaVictims": {f"f{i:03d}": {"pods": []} for i in range(40)}})))["nodeNameToMetaVictims"]
+    assert 1 <= len(plans) <= 4 and "f005" not in plans and "f017" not in plans
+    assert all(len(v["pods"]) == 1 for v in plans.values())
+
+
+def test_request_waits_for_a_job_that_is_about_to_finish_instead_of_preempting():
+    p = Platform({"scheduler": {"preemptionWaitWindowSeconds": 30, "preemptionMaxWaitSeconds": 0.3,
+                                "preemptionUrgentPriority": 1000}})
+    p.add_fake_node(make_fixture("w0", 8, 2))
+    assert p.schedule(wl("ending", 8, priority=1, expectedDurationSeconds=5))["ok"]
+    d = p.schedule(wl("hi", 8, priority=100))
+    assert not d["ok"]                                       # told to wait: nothing evicted
+    m = p.scheduler_metrics()
+    assert m["preemptions"] == 0 and m["preemptions_deferred_wait"] == 1
+    assert _alloc(p, "ending") is not None
+    # an urgent request does not wait
+    u = p.schedule(wl("urgent", 8, priority=1000))
+    assert u["ok"] and u["preempted"] == ["ending"]
+    # and patience runs out: past preemptionMaxWaitSeconds the waiting request preempts too
+    assert p.release("urgent")
+    assert p.schedule(wl("ending2", 8, priority=1, expectedDurationSeconds=5))["ok"]
+    assert not p.schedule(wl("hi2", 8, priority=100))["ok"]
+    import time
+    time.sleep(0.4)
+    d = p.schedule(wl("hi2", 8, priority=100))
+    assert d["ok"] and d["preempted"] == ["ending2"]
+
+
+def test_long_running_victims_are_preempted_while_near_finishers_are_spared():
+    p = Platform({"scheduler": {"preemptionWaitWindowSeconds": 30}})
+    p.add_fake_node(make_fixture("w0", 8, 2))
+    assert p.schedule(wl("long1", 3, priority=1, expectedDurationSeconds=86400))["ok"]
+    assert p.schedule(wl("long2", 3, priority=1, expectedDurationSeconds=86400))["ok"]
+    assert p.schedule(wl("short", 2, priority=1, expectedDurationSeconds=5))["ok"]   # youngest: first in line otherwise
+    d = p.schedule(wl("hi", 4, priority=100))   # the near finisher's 2 GPUs are not enough to wait for
+    assert d["ok"] and sorted(d["preempted"]) == ["long1", "long2"]
+    assert _alloc(p, "short") is not None
+
+
+def test_preemption_rate_window_caps_victims_and_counts_refusals():
+    p = Platform({"scheduler": {"preemptionWaitWindowSeconds": 0, "preemptionMaxRatePercent": 5.0,
+                                "preemptionBurst": 2, "preemptionWindowSeconds": 60}})
+    _full_fleet(p, 6)
+    got = [p.schedule(wl(f"hi{i}", 8, priority=100)) for i in range(4)]
+    assert [d["ok"] for d in got] == [True, True, False, False]     # burst of 2, then 5 % of ~8 placements = 0
+    m = p.scheduler_metrics()
+    assert m["preemptions"] == 2 and m["preemptions_rate_limited"] == 2
+    # no cap configured: everything preempts
+    q = Platform({"scheduler": {"preemptionWaitWindowSeconds": 0, "preemptionMaxRatePercent": 0}})
+    _full_fleet(q, 6)
+    assert all(q.schedule(wl(f"hi{i}", 8, priority=100))["ok"] for i in range(4))
+
+
+def test_lifetimes_are_learned_per_workload_type_when_not_declared():
+    p = Platform({})
+    p.add_fake_node(make_fixture("l0", 8, 2))
+    for i in range(8):
+        assert p.schedule(wl(f"s{i}", 1))["ok"]
+        assert _alloc(p, f"s{i}")["expected_duration_s"] == 0     # nothing learned yet
+        assert p.release(f"s{i}")
+    assert p.schedule(wl("next", 1))["ok"]
+    a = _alloc(p, "next")
+    assert 0 < a["expected_duration_s"] < 5       # the observed (milliseconds-long) lifetimes
+    import time
+    assert abs(a["allocated_unix_s"] - time.time()) < 5
+    assert p.schedule(wl("decl", 1, expectedDurationSeconds=3600))["ok"]
+    a = _alloc(p, "decl")
+    assert abs(a["expected_duration_s"] - 3600) < 1e-6

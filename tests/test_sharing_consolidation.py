@@ -212,6 +212,70 @@ def test_consolidation_hysteresis_waits():
     assert len(p.consolidate_partitions(1101.0, plan_only=True)) == 1
 
 
+def test_plan_only_consolidation_bars_new_slices_on_the_donor_until_it_is_empty():
+    """Controller path on two nodes: the plan names the moves, the caller
+    evicts the donor's pods.  Until the donor is empty and back to SPX no new
+    slice may land on it, so the evicted pods reschedule onto the receiver."""
+    p = Platform({"enforceBudgets": False, "partitionReclaimIdleSeconds": -1,
+                  "partitionConsolidateAfterSeconds": 0, "migrationCooldownSeconds": 0})
+    for n in ("n0", "n1"):
+        p.add_fake_node(make_fixture(n, 8, 2))
+    for k in range(7):   # n0 keeps one GPU free: the first CPX GPU is there, the second on n1
+        w = whole_wl(f"fill{k}", 1, topo="None")
+        w["spec"]["constraints"] = {"nodeSelector": {"kubernetes.io/hostname": "n0"}}
+        assert p.schedule(w)["ok"]
+    for n in ("n0", "n1"):
+        for k in range(8):
+            d = p.schedule(cpx_wl(f"{n}-i{k}"))
+            assert d["ok"] and d["node"] == n
+    for k in range(2, 8):
+        p.release(f"n0-i{k}")      # n0's GPU: 2 of 8 used
+    for k in range(5, 8):
+        p.release(f"n1-i{k}")      # n1's GPU: 5 of 8 used
+    moves = p.consolidate_partitions(time.time(), plan_only=True)
+    assert sorted(m["uid"] for m in moves) == ["n0-i0", "n0-i1"]
+    assert all(m["node_from"] == "n0" and m["node_to"] == "n1" for m in moves)
+    donor = moves[0]["from"].rsplit("/p", 1)[0]
+    assert p.draining_gpus() == [donor]
+    # the ledger is untouched by a plan, but the donor takes no new slice: a fresh
+    # request that would otherwise pack onto n0's 6 free slices goes to n1
+    assert len(p.allocations()) == 7 + 7
+    d = p.schedule(cpx_wl("fresh"))
+    assert d["ok"] and d["node"] == "n1"
+    # the caller evicts the two pods; they come back and land on the receiver
+    for m in moves:
+        assert p.release(m["uid"])
+        d = p.schedule(cpx_wl(m["uid"] + "-again"))
+        assert d["ok"] and d["node"] == "n1" and not d["partitions"][0].startswith(donor)
+    # donor empty: the next pass returns it to SPX and lifts the bar
+    p.consolidate_partitions(time.time(), plan_only=True)
+    assert p.draining_gpus() == []
+    m = p.partition_metrics()
+    assert m["modes"]["CPX"]["gpus"] == 1
+
+
+def test_a_donor_that_never_empties_is_given_back():
+    p = Platform({"enforceBudgets": False, "partitionReclaimIdleSeconds": -1,
+                  "partitionConsolidateAfterSeconds": 0, "migrationCooldownSeconds": 0})
+    p.add_fake_node(make_fixture("n0", 8, 2))
+    for k in range(16):
+        assert p.schedule(cpx_wl(f"i{k}"))["ok"]
+    by_gpu = {}
+    for a in p.allocations():
+        by_gpu.setdefault(a["partitions"][0].rsplit("/p", 1)[0], []).append(a["uid"])
+    (ga, ua), (gb, ub) = sorted(by_gpu.items())
+    for u in ua[2:] + ub[5:]:
+        p.release(u)
+    t0 = 1000.0
+    assert len(p.consolidate_partitions(t0, plan_only=True)) == 2
+    assert p.draining_gpus() == [ga]
+    assert p.consolidate_partitions(t0 + 200, plan_only=True) == [] and p.draining_gpus() == [ga]
+    p.consolidate_partitions(t0 + 301, plan_only=True)   # nobody evicted the pods: bar lifted, planned again
+    assert ga in p.draining_gpus() or p.draining_gpus() == []
+    held_on_a = [a for a in p.allocations() if a["partitions"][0].startswith(ga)]
+    assert len(held_on_a) == 2
+
+
 def test_bind_records_pod_latency_and_queue_depth(plat):
     names = [f"p{i}" for i in range(5)]
     for n in names:
@@ -261,3 +325,20 @@ def test_restore_keeps_preemptible_type_gang_and_share():
     # and the restored share still blocks whole-GPU use of its GPU
     d1 = p.schedule(whole_wl("w1", 1, prio=0, topo="None"))
     assert not d1["ok"] or "GPU-n0-01" not in d1["gpus"]
+
+
+def test_share_placement_counts_hbm_the_device_reports_in_use():
+    """A co-located client's HBM cap must fit next to what the device itself
+    reports as used, not only next to the caps the ledger promised."""
+    node = make_fixture("m0", 2, 1)
+    node["gpus"][0]["memory_used_gb"] = 270.0      # somebody outside the ledger holds 270 of 288 GB
+    p = Platform({"enforceBudgets": False})
+    p.upsert_node(node)
+    busy, free = node["gpus"][0]["uuid"], node["gpus"][1]["uuid"]
+    for k in range(8):      # eight 30 GB clients fill the other GPU's client slots
+        d = p.schedule(share_wl(f"c{k}", mem=30.0))
+        assert d["ok"] and d["shared_gpu"] == free
+    # only the busy GPU is left: 270 + 30 > 288 is refused, 270 + 10 fits
+    assert not p.schedule(share_wl("big", mem=30.0))["ok"]
+    d = p.schedule(share_wl("small", mem=10.0))
+    assert d["ok"] and d["shared_gpu"] == busy

@@ -20,6 +20,7 @@
 #   ops                   tools/ops_bench.py (every hand-written op against its roofline)
 #   infer N [args]        co-location bench with N clients (kgwe.bench.infer colocate)
 #   sched [args]          extender latency bench (kgwe.bench.sched_latency)
+#   sched-suite           the seven latency / pressure runs reported under profiles/*_sched/
 #   probe-pmc             counter validation of the HBM / LDS probe kernels
 #   ab VAR=VALUE [bench args]
 #                         the training bench with VAR=VALUE set, then without, twice over, on
@@ -121,6 +122,25 @@ EOF
 sched)
   run 900 gpurun_out/sched.log python -m kgwe.bench.sched_latency "$@"
   tail -1 gpurun_out/sched.log | cut -c1-3000 ;;
+sched-suite)
+  # The extender latency runs that profiles/*_sched/ reports (CPU only; run on the
+  # GPU box because its cores are the ones the driver's bench runs on).
+  mkdir -p gpurun_out/sched
+  one() { # name args...
+    local name=$1; shift
+    echo "== $name: $*"
+    timeout -k 10 900 python -m kgwe.bench.sched_latency --json --timeout 700 "$@" \
+      > "gpurun_out/sched/$name.json" 2> "gpurun_out/sched/$name.err" || { tail -5 "gpurun_out/sched/$name.err"; exit 1; }
+    python tools/sched_brief.py "gpurun_out/sched/$name.json"
+  }
+  one scale_1250n_names_50pps   --pods 3000 --nodes 1250 --rate 50 --node-cache
+  one scale_1250n_names_100pps  --pods 5000 --nodes 1250 --rate 100 --node-cache
+  one scale_1250n_full_10pps    --pods 600 --nodes 1250 --rate 10 --full-nodes
+  one scale_64n_names_50pps     --pods 2000 --nodes 64 --rate 50 --node-cache
+  one pressure_64n              --pods 2000 --nodes 64 --rate 50 --lifetime 5,15 --node-cache
+  one pressure_1250n            --pods 10000 --nodes 1250 --rate 100 --lifetime 32,64 --node-cache
+  one pressure_1250n_2x         --pods 8000 --nodes 1250 --rate 100 --lifetime 60,120 --node-cache
+  ;;
 probe-pmc)
   rocprof_env
   run 120 gpurun_out/probe_plain.log python3 tools/probe_pmc.py run
