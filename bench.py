@@ -50,8 +50,8 @@ import json
 import os
 import sys
 
-BASELINE_UTIL = 87.0      # KGWE avg GPU utilisation (H100 DGX)
-BASELINE_P99_MS = 85.0    # KGWE p99 scheduling latency
+BASELINE_UTIL = 87.0      # reference README.md:157-160: KGWE avg GPU utilisation (H100 DGX)
+BASELINE_P99_MS = 85.0    # reference docs/PRD.md:440: KGWE p99 scheduling latency
 MI355X_BF16_DENSE = 2.5e15
 METRIC = ("p99 scheduling latency (ms) + avg GPU-util %, 8-GPU FSDP job on one "
           "MI355X node")

@@ -125,7 +125,7 @@ def build_core(force: bool = False, jobs: int = 8) -> Path | None:
     cxx = os.environ.get("CXX", "g++")
     flags, link = list(CXX_FLAGS), ["-ldl", "-lpthread"]
     if os.environ.get("KGWE_CORE_SANITIZE") == "1":
-        # Host-only ASan + UBSan build of the platform core (the
+        # Host-only ASan + UBSan build of the platform core (the role of the
         # reference's `go test -race`); load with LD_PRELOAD=libasan.so.
         san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
         flags += san
@@ -146,7 +146,7 @@ SANITIZERS = {
 def build_native_tests(flavour: str = "plain", force: bool = False, jobs: int = 8) -> Path:
     """Standalone C++ test binary over the platform core (no pybind11, no
     Python): ``build/tests/core_tests_<flavour>``.  ``tsan`` / ``asan`` are
-    the host-side race / memory-error builds (SURVEY.md §5.2)."""
+    the host-side race / memory-error builds."""
     core_dir = ROOT / "native" / "core"
     test_dir = ROOT / "native" / "tests"
     srcs = [s for s in sorted(core_dir.glob("*.cpp")) if s.name != "bindings.cpp"]

@@ -69,7 +69,12 @@ GPUWORKLOAD_SPEC = _S(
                                          default="CoLocate"),
                             "cuPercent": _S(type="number", minimum=0, maximum=100,
                                             description="Share of the GPU's 256 CUs (12.5 = one XCD)"),
-                            "memoryGB": _S(type="number", minimum=0, maximum=288)}),
+                            "memoryGB": _S(type="number", minimum=0, maximum=288),
+                            "group": _S(type="string", maxLength=63, pattern="^[A-Za-z0-9._-]*$", description=(
+                                "Share group: workloads of one group on a GPU (same model) hold ONE CU range "
+                                "and ONE HBM cap, sized by the group's first workload (its leader, which runs "
+                                "the serving process, python -m kgwe.serving.batch_server); the others connect "
+                                "to it through KGWE_BATCH_ENDPOINT and add no weights of their own."))}),
             "mig": _S(type="object", description="Deprecated: mapped to partition",
                       properties={"profile": _S(type="string"), "count": _S(type="integer", minimum=1)}),
             "gpuModel": _S(type="string", description="e.g. MI355X"),
@@ -85,6 +90,10 @@ GPUWORKLOAD_SPEC = _S(
                                   description="Model size hint for the optimizer's rightsizing"),
         "priority": _S(type="integer", minimum=0, maximum=1000000, default=0),
         "preemptible": _S(type="boolean", default=True),
+        "expectedDurationSeconds": _S(type="number", minimum=0, description=(
+            "How long the workload expects to hold its GPUs; preemption spares a job within the wait window "
+            "of its expected end and waits for it instead (reference WorkloadSpec.EstimatedDuration, "
+            "src/scheduler/types.go:92-110, never read there).")),
         "team": _S(type="string"),
         "project": _S(type="string"),
         "gang": _S(type="object", properties={"name": _S(type="string"),

@@ -1,6 +1,6 @@
 """Validating / mutating admission webhook for kgwe custom resources
 (reference: declared only — values.yaml:375-392 cert-manager webhook with
-failurePolicy Fail, Makefile:111 controller-gen webhook; SURVEY.md D8).
+failurePolicy Fail, Makefile:111 controller-gen webhook).
 
 `review()` takes an admission.k8s.io/v1 AdmissionReview and returns the
 response AdmissionReview: the validating path rejects schema / semantic

@@ -5,6 +5,8 @@ reference README.md:31 "7x GPU density").
 ``run``       one decode client: build a random-init Llama (bf16), prefill a
               synthetic prompt, capture the decode step in a hipGraph, then
               time ``--new`` greedy decode steps.  Prints one JSON line.
+``client``    one client of a share group's batch server (no GPU in this
+              process): waits for the go file, sends its prompt, streams tokens.
 ``colocate``  the platform path end to end on the local GPU: the C++
               scheduler ledger places ``--clients`` CoLocate shares on the
               GPU (``Platform.schedule`` of GPUWorkload-shaped requests ->
@@ -15,6 +17,10 @@ reference README.md:31 "7x GPU density").
               aggregate tokens/s, against (a) one client alone on the whole
               GPU and (b) one process decoding the clients' combined batch.
               The parent never touches the GPU (no HIP call): it only spawns.
+              ``--share-mode batched``: the clients are ONE share group — the
+              ledger gives the group one CU range and one HBM cap, the leader's
+              env starts ``kgwe.serving.batch_server`` (weights once, continuous
+              batching), and every client talks to it over the group's socket.
 """
 from __future__ import annotations
 
@@ -83,6 +89,32 @@ def run_client(a) -> dict:
             "last_tokens": gen.tok[:4].tolist()}
 
 
+def run_group_client(a) -> dict:
+    """A member of a share group: tokens come from the group's server."""
+    import random
+
+    from ..serving import client
+
+    rnd = random.Random(a.seed)
+    prompt = [[rnd.randrange(0, a.vocab) for _ in range(a.prompt)] for _ in range(a.batch)]
+    sock = client.connect(a.endpoint or None, timeout=a.timeout)
+    if a.ready_file:
+        open(a.ready_file, "w").close()
+        while not os.path.exists(a.go_file):
+            time.sleep(0.005)
+        go = float(open(a.go_file).read().strip() or 0)
+        while time.time() < go:
+            pass
+    r = client.generate(prompt, a.new, sock=sock, timeout=a.timeout)
+    sock.close()
+    toks = a.batch * (a.new - 1)  # the tokens after the prefill's, as run_client counts them
+    dt = r["t_end"] - r["t_first"]
+    return {"batch": a.batch, "prompt": a.prompt, "new_tokens": a.new, "tokens": toks,
+            "t_submit": r["t_submit"], "t_start": r["t_first"], "t_end": r["t_end"], "decode_s": dt,
+            "tokens_per_s": toks / dt, "step_ms": 1000 * dt / (a.new - 1),
+            "ttft_s": r["t_first"] - r["t_submit"], "last_tokens": [row[-1] for row in r["tokens"]][:4]}
+
+
 # --------------------------------------------------------------------------- parent
 def _client_cmd(a, batch: int) -> list[str]:
     return [sys.executable, "-m", "kgwe.bench.infer", "run", "--model", a.model, "--batch", str(batch),
@@ -99,12 +131,13 @@ def _run_alone(a, batch: int, env: dict | None = None) -> dict:
     return json.loads(js[-1])
 
 
-def place_shares(n: int, cu_percent: float, memory_gb: float) -> tuple[list[dict], str]:
+def place_shares(n: int, cu_percent: float, memory_gb: float, group: str = "",
+                 socket_dir: str = "") -> tuple[list[dict], str]:
     """Shares from the real scheduler ledger: the local GPU via amd-smi when
-    present (else a mocked MI355X node)."""
+    present (else a mocked MI355X node).  group: all n are one share group."""
     from ..core import Platform, amdsmi_discover, make_fixture
 
-    p = Platform({"enforceBudgets": False})
+    p = Platform(dict({"enforceBudgets": False}, **({"shareSocketDir": socket_dir} if socket_dir else {})))
     src = "amd-smi"
     d = amdsmi_discover("local")
     if d.get("ok") and (d.get("node") or {}).get("gpus"):
@@ -119,6 +152,8 @@ def place_shares(n: int, cu_percent: float, memory_gb: float) -> tuple[list[dict
                       "gpuRequirements": {"count": 1, "sharing": {"method": "CoLocate",
                                                                    "cuPercent": cu_percent,
                                                                    "memoryGB": memory_gb}}}}
+        if group:
+            w["spec"]["gpuRequirements"]["sharing"]["group"] = group
         dd = p.schedule(w)
         if not dd.get("ok"):
             raise RuntimeError(f"share {i} not placed: {dd.get('failed_nodes')}")
@@ -126,7 +161,102 @@ def place_shares(n: int, cu_percent: float, memory_gb: float) -> tuple[list[dict
     return out, src
 
 
+def _wait_ready(paths: list[str], procs: list, deadline: float, what: str) -> None:
+    while not all(os.path.exists(p) for p in paths):
+        if time.time() > deadline or any(p.poll() not in (None, 0) for p in procs):
+            for p in procs:
+                p.kill()
+            errs = [p.communicate()[1][-800:] for p in procs if p.returncode not in (None, 0)]
+            raise RuntimeError(f"{what} did not get ready: {errs[:2]}")
+        time.sleep(0.05)
+
+
+def colocate_batched(a) -> dict:
+    """--share-mode batched: one share group, one serving process."""
+    from ..models import llama
+
+    tmp = tempfile.mkdtemp(prefix="kgwe-group-")
+    shares, src = place_shares(a.clients, a.cu_percent, a.memory_gb, group=a.model, socket_dir=tmp)
+    lead = [s for s in shares if s.get("share_leader")]
+    assert len(lead) == 1 and all(s["shared_gpu"] == lead[0]["shared_gpu"] for s in shares), shares
+    endpoint = lead[0]["env"]["KGWE_BATCH_ENDPOINT"]
+    res: dict = {"mode": "batched", "clients": a.clients, "model": a.model, "batch_per_client": a.batch,
+                 "prompt": a.prompt, "new_tokens": a.new, "topology_source": src,
+                 "shared_gpus": sorted({s["shared_gpu"] for s in shares}),
+                 "cu_masks": sorted({s["env"]["HSA_CU_MASK"] for s in shares}),
+                 "roles": [s["env"]["KGWE_SHARE_ROLE"] for s in shares],
+                 "hbm_cap": lead[0]["env"].get("KGWE_GPU_MEMORY_FRACTION")}
+    if not a.skip_baselines:
+        res["alone"] = _run_alone(a, a.batch)
+    env = dict(os.environ)
+    env.update(lead[0]["env"])
+    env["HIP_VISIBLE_DEVICES"] = env["ROCR_VISIBLE_DEVICES"] = "0"
+    from ..launch import enforce_share_limits
+
+    enforce_share_limits(env)  # what `python -m kgwe.launch` does in the pod
+    server = subprocess.Popen(
+        [sys.executable, "-m", "kgwe.serving.batch_server", "--model", a.model, "--slots", str(a.clients),
+         "--rows", str(a.batch), "--max-seq", str(a.prompt + a.new + 1), "--flush", str(a.flush),
+         "--ready-file", f"{tmp}/server-ready"],
+        cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    deadline = time.time() + a.timeout
+    try:
+        _wait_ready([f"{tmp}/server-ready"], [server], deadline, "batch server")
+        vocab = llama.PRESETS[a.model].vocab_size
+        procs = []
+        for i, s in enumerate(shares):
+            cenv = dict(os.environ)
+            cenv.update({k: v for k, v in s["env"].items() if k.startswith("KGWE_")})
+            cenv["HIP_VISIBLE_DEVICES"] = cenv["ROCR_VISIBLE_DEVICES"] = ""  # a member never opens the GPU
+            cmd = [sys.executable, "-m", "kgwe.bench.infer", "client", "--batch", str(a.batch),
+                   "--prompt", str(a.prompt), "--new", str(a.new), "--seed", str(a.seed + i), "--vocab", str(vocab),
+                   "--endpoint", endpoint, "--ready-file", f"{tmp}/ready{i}", "--go-file", f"{tmp}/go",
+                   "--timeout", str(a.timeout), "--json"]
+            procs.append(subprocess.Popen(cmd, cwd=ROOT, env=cenv, stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True))
+        _wait_ready([f"{tmp}/ready{i}" for i in range(a.clients)], procs + [server], deadline, "group clients")
+        with open(f"{tmp}/go.tmp", "w") as f:
+            f.write(f"{time.time() + 0.5:.6f}")
+        os.replace(f"{tmp}/go.tmp", f"{tmp}/go")
+        clients = []
+        for p in procs:
+            out, err = p.communicate(timeout=a.timeout)
+            js = [ln for ln in out.splitlines() if ln.startswith("{")]
+            if p.returncode != 0 or not js:
+                raise RuntimeError(f"group client failed rc={p.returncode}: {err[-1500:]}")
+            clients.append(json.loads(js[-1]))
+        from ..serving import client as sc
+
+        res["server"] = sc.call(endpoint, {"op": "stats"})
+        sc.call(endpoint, {"op": "shutdown"})
+        server.communicate(timeout=30)
+    finally:
+        if server.poll() is None:
+            server.kill()
+    t0 = min(c["t_start"] for c in clients)
+    t1 = max(c["t_end"] for c in clients)
+    toks = sum(c["tokens"] for c in clients)
+    agg = toks / (t1 - t0)
+    res.update({
+        "per_client_tokens_per_s": [round(c["tokens_per_s"], 1) for c in clients],
+        "per_client_step_ms": [round(c["step_ms"], 3) for c in clients],
+        "per_client_ttft_ms": [round(1000 * c["ttft_s"], 1) for c in clients],
+        "aggregate_tokens_per_s": round(agg, 1),
+        # from the first submit to the last token: prefill of all eight included
+        "aggregate_tokens_per_s_incl_prefill": round(
+            sum(c["tokens"] + c["batch"] for c in clients) / (t1 - min(c["t_submit"] for c in clients)), 1),
+        "memory_caps_applied": bool(res["server"].get("peak_mem_gb", 0) > 0 and res["hbm_cap"]),
+        "server_peak_mem_gb": round(res["server"].get("peak_mem_gb", 0.0), 2),
+    })
+    if not a.skip_baselines:
+        alone = res["alone"]["tokens_per_s"]
+        res.update({"alone_tokens_per_s": round(alone, 1), "density_vs_alone": round(agg / alone, 3)})
+    return res
+
+
 def colocate(a) -> dict:
+    if a.share_mode == "batched":
+        return colocate_batched(a)
     shares, src = place_shares(a.clients, a.cu_percent, a.memory_gb)
     gpus = {s["shared_gpu"] for s in shares}
     masks = [s["env"]["HSA_CU_MASK"] for s in shares]
@@ -196,7 +326,7 @@ def colocate(a) -> dict:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="kgwe bench-infer")
-    ap.add_argument("mode", choices=["run", "colocate"])
+    ap.add_argument("mode", choices=["run", "colocate", "client"])
     ap.add_argument("--model", default="llama3.2-1b")
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--prompt", type=int, default=512)
@@ -215,8 +345,14 @@ def main(argv=None) -> int:
     ap.add_argument("--ready-file", default="")
     ap.add_argument("--go-file", default="")
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--share-mode", default="processes", choices=["processes", "batched"],
+                    help="processes: one process (and one copy of the weights) per client, disjoint CU masks; "
+                         "batched: the clients are one share group behind one serving process")
+    ap.add_argument("--flush", type=int, default=16, help="batched: decode steps per token hand-out")
+    ap.add_argument("--endpoint", default="", help="client: the group server's address")
+    ap.add_argument("--vocab", type=int, default=32000, help="client: vocabulary size for the synthetic prompt")
     a = ap.parse_args(argv)
-    out = run_client(a) if a.mode == "run" else colocate(a)
+    out = run_client(a) if a.mode == "run" else run_group_client(a) if a.mode == "client" else colocate(a)
     print(json.dumps(out) if a.json else json.dumps(out, indent=1), flush=True)
     return 0
 

@@ -1,7 +1,6 @@
 """In-process fake kube-apiserver (nodes, pods + binding, events, kgwe CRDs).
 
-Stands in for a cluster where kind / kubectl / Go are absent (SURVEY.md §7.5
-hard part 5): it speaks enough of the Kubernetes REST surface — list / get /
+Stands in for a cluster where kind / kubectl / Go are absent: it speaks enough of the Kubernetes REST surface — list / get /
 create / merge-patch / delete, the pods/binding subresource, CR status
 subresources and a long-poll watch — for the controller, the extender and the
 kube-scheduler simulator to run unchanged against it, over real HTTP.

@@ -1,8 +1,7 @@
 """Node labels derived from a pushed MI355X node topology.
 
 Reference: the discovery service declares ``UpdateNodeLabels`` on its
-Kubernetes client interface but never calls it (src/discovery/discovery.go:82,
-SURVEY D15).  Here the controller (lease holder) labels each node whenever the
+Kubernetes client interface but never calls it (src/discovery/discovery.go:82).  Here the controller (lease holder) labels each node whenever the
 agent's topology push changes a label, so ordinary nodeSelectors / affinities
 (and the GPUWorkload ``constraints.nodeSelector``) can target hardware facts:
 GPU model/arch/count/HBM size, whether the 8 GPUs form one fully connected xGMI

@@ -2,7 +2,7 @@
 
 Reference: leader-election settings only (values.yaml:65-71 lease 15 s /
 renew 10 s / retry 2 s; scheduler-configmap.yaml:14-17) with 2 replicas and an
-in-memory ledger that would diverge between them (SURVEY.md §5.3).  Here
+in-memory ledger that would diverge between them.  Here
 only the lease holder runs the reconcilers and serves mutating extender
 verbs; a follower that takes over rebuilds the ledger from pod annotations
 (Reconciler.rebuild_ledger), so the apiserver stays the single source of

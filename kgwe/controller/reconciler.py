@@ -1,6 +1,6 @@
 """Controller reconcile loops for GPUWorkload / GPUBudget / PartitionStrategy.
 
-Reference: the designed flow (docs/architecture.md:139-168; SURVEY.md §3g) —
+Reference: the designed flow (docs/architecture.md:139-168) —
 "[controller] reconciles CR -> creates Pod(schedulerName=kgwe-scheduler,
 podTemplate)", writes GPUWorkload.status, starts/stops cost tracking — none of
 which exists in the reference (D1).  Here:
@@ -13,14 +13,14 @@ which exists in the reference (D1).  Here:
 * Pod termination / deletion -> allocation release + cost finalisation.
 * GPUBudget -> cost-engine budget; status (spend, utilisation, alerts).
 * PartitionStrategy -> registered + rebalanced every rebalanceInterval.
-* Failure detection / recovery (SURVEY.md §5.3; the reference only evicts a
+* Failure detection / recovery (the reference only evicts a
   deleted node from its cache and leaves its allocations stale): a node that
   is deleted or stops being Ready, or a GPU of a running allocation that the
   amd-smi health policy marks Unhealthy, evicts the workloads on it — the
   allocation is released and, per ``spec.recovery`` (Reschedule, at most
   maxRestarts times), the GPUWorkload gets a fresh pod that the scheduler
   places elsewhere; status carries ``restarts`` / ``lastFailure``.
-* Restart safety (checkpoint/resume): on start the ledger is
+* Restart safety: on start the ledger is
   rebuilt from the full allocation annotation of already-bound pods
   (priority, preemptible, type, gang, share CU range included), so a
   controller restart or leader change neither leaks GPUs nor turns a
@@ -268,10 +268,15 @@ class Reconciler:
             # a preempted gang member: the gang goes as a unit (the extender's
             # preempt verb can only name the victims on the preemptor's node)
             peers = set(rel.get("evict_gang_peers") or [])
-            if peers:
+            # a share group's leader: its members connected to the serving process that
+            # just went away; evicted, they reschedule and the first becomes the new leader
+            orphans = set(rel.get("orphaned_share_members") or [])
+            if peers or orphans:
                 for a in self.p.allocations():
                     if a["uid"] in peers:
                         self.evict(a, f"gang member {uid} preempted")
+                    elif a["uid"] in orphans:
+                        self.evict(a, f"share group leader {uid} is gone")
             run = self._running.pop(uid, None)
             if run and self.optimizer is not None and uid not in self._evicting:
                 try:  # a finished run -> a training row of the online model

@@ -7,6 +7,11 @@ parses that file, exports HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES, the
 RCCL rendezvous (MASTER_ADDR/PORT, WORLD_SIZE, NPROC_PER_NODE) and NCCL_*
 tuning, then replaces itself with <cmd> (typically torchrun).  It execs
 BEFORE anything touches the GPU, so the exec is safe.
+
+A co-located share's HBM cap (KGWE_GPU_MEMORY_FRACTION) is enforced, not just
+exported: the launcher puts ``kgwe/_sitehook`` first on PYTHONPATH, whose
+``sitecustomize`` caps PyTorch's allocator in every Python process of the
+workload as soon as that process imports torch.
 """
 from __future__ import annotations
 
@@ -16,6 +21,20 @@ import sys
 
 ANN_FILE = os.environ.get("KGWE_ANNOTATIONS_FILE", "/etc/kgwe/annotations")
 ANN_ENV = "kgwe.amd.com/rccl-env"
+SITEHOOK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_sitehook")
+
+
+def enforce_share_limits(env: dict) -> dict:
+    """With an HBM cap in the placement, make every Python process of the
+    workload install it at start-up (see kgwe/_sitehook/sitecustomize.py)."""
+    try:
+        frac = float(env.get("KGWE_GPU_MEMORY_FRACTION", "0") or 0)
+    except ValueError:
+        frac = 0.0
+    if 0.0 < frac < 1.0:
+        parts = [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p and p != SITEHOOK]
+        env["PYTHONPATH"] = os.pathsep.join([SITEHOOK] + parts)
+    return env
 
 
 def parse_downward_api(text: str) -> dict:
@@ -54,6 +73,7 @@ def main(argv=None) -> int:
     except FileNotFoundError:
         print(f"[kgwe.launch] {ANN_FILE} not found: running without a kgwe placement",
               file=sys.stderr)
+    enforce_share_limits(env)
     os.execvpe(argv[0], argv, env)
     return 127  # not reached
 

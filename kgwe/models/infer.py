@@ -45,6 +45,9 @@ class Generator:
         self.tok = torch.zeros(batch, dtype=torch.long, device=self.dev)
         self.pos = torch.zeros(batch, dtype=torch.int32, device=self.dev)
         self.lens = torch.zeros(batch, dtype=torch.int32, device=self.dev)
+        # 1 = the row decodes; 0 = the row is idle (its position does not
+        # advance, so an unused slot of a serving batch never runs off the cache)
+        self.active = torch.ones(batch, dtype=torch.int32, device=self.dev)
         self.graph = None
         self.filled = 0  # host-side count of cached positions (no device sync)
         # Fused decode projections (native/ops/gemv.hip): RMSNorm + residual,
@@ -60,12 +63,17 @@ class Generator:
 
     # ------------------------------------------------------------ prefill
     @torch.no_grad()
-    def prefill(self, tokens: torch.Tensor) -> torch.Tensor:
-        """tokens [B, P] -> next token [B]; fills cache positions [0, P)."""
+    def prefill(self, tokens: torch.Tensor, rows: tuple[int, int] | None = None) -> torch.Tensor:
+        """tokens [B, P] -> next token [B]; fills cache positions [0, P).
+        With rows=(r0, r1) only batch rows [r0, r1) are prefilled (tokens
+        [r1 - r0, P]); the other rows' cache, tokens and positions are left as
+        they are, so a serving loop admits a request between two decode steps."""
         c, m = self.cfg, self.m
         B, P = tokens.shape
-        if B != self.B or P >= self.smax:
-            raise ValueError(f"prefill: expected [B={self.B}, P<{self.smax}], got {tuple(tokens.shape)}")
+        r0, r1 = rows if rows is not None else (0, self.B)
+        if not (0 <= r0 < r1 <= self.B) or B != r1 - r0 or P >= self.smax:
+            raise ValueError(f"prefill: expected [B={r1 - r0}, P<{self.smax}] for rows {r0}:{r1} of {self.B}, "
+                             f"got {tuple(tokens.shape)}")
         hq, hkv, d = c.n_heads, c.n_kv_heads, c.head_dim
         cos, sin = self.cos[:P], self.sin[:P]
         h = m.tok_embeddings(tokens)
@@ -78,21 +86,21 @@ class Generator:
             qkv = K.linear(xn, layer.attention.wqkv).view(B * P, -1)
             q, k, v = K.rope_qkv(qkv, cos, sin, P, hq, hkv, d)
             k4, v4 = k.view(B, P, hkv, d), v.view(B, P, hkv, d)
-            self.kv[0, i, :, :, :P].copy_(k4.transpose(1, 2))
-            self.kv[1, i, :, :, :P].copy_(v4.transpose(1, 2))
+            self.kv[0, i, r0:r1, :, :P].copy_(k4.transpose(1, 2))
+            self.kv[1, i, r0:r1, :, :P].copy_(v4.transpose(1, 2))
             o = attn_ops.attention(q.view(B, P, hq, d), k4, v4, causal=True)
             a = K.linear(o.reshape(B, P, -1), layer.attention.wo)
             xn, residual = K.rmsnorm(a, layer.ffn_norm, c.norm_eps, residual=residual)
             h = layer.feed_forward(xn)
         h, _ = K.rmsnorm(h, m.norm, c.norm_eps, residual=residual)
         logits = K.linear(h[:, -1], m.output)
-        if self.keep_logits:
+        if self.keep_logits and rows is None:
             self.logits = logits.clone()
         nxt = logits.argmax(-1)
-        self.tok.copy_(nxt)
-        self.pos.fill_(P)
-        self.lens.fill_(P + 1)
-        self.filled = P
+        self.tok[r0:r1].copy_(nxt)
+        self.pos[r0:r1].fill_(P)
+        self.lens[r0:r1].fill_(P + 1)
+        self.filled = max(P, self.filled) if rows is not None else P
         return nxt
 
     # ------------------------------------------------------------ decode
@@ -126,8 +134,8 @@ class Generator:
         dec.gemv(x, m.output, dec.GEMV_NORM_ARGMAX, res=res, g=m.norm, eps=eps,
                  y=self.logits if self.keep_logits else None, best=self.best)
         dec.argmax_finish(self.best, self.tok)
-        self.pos.add_(1)
-        self.lens.add_(1)
+        self.pos.add_(self.active)
+        self.lens.add_(self.active)
 
     @torch.no_grad()
     def _step(self) -> None:
@@ -155,8 +163,8 @@ class Generator:
                 self.logits = torch.empty_like(logits)
             self.logits.copy_(logits)
         self.tok.copy_(logits.argmax(-1))
-        self.pos.add_(1)
-        self.lens.add_(1)
+        self.pos.add_(self.active)
+        self.lens.add_(self.active)
 
     def capture(self) -> None:
         """Record one decode step in a hipGraph (warm-up on a side stream, as
@@ -178,8 +186,19 @@ class Generator:
         self.graph = g
         # capture does not execute the work: state is unchanged
 
-    def step(self) -> torch.Tensor:
-        if self.filled + 1 >= self.smax:
+    def idle_rows(self, r0: int, r1: int, idle: bool = True) -> None:
+        """Park batch rows [r0, r1) (or wake them): a parked row keeps decoding
+        position 0 of its own cache slab and is ignored by the caller."""
+        self.active[r0:r1].fill_(0 if idle else 1)
+        if idle:
+            self.pos[r0:r1].zero_()
+            self.lens[r0:r1].fill_(1)
+
+    def step(self, check: bool = True) -> torch.Tensor:
+        """One decode step for every row.  check=False: the caller tracks each
+        row group's length itself (a serving loop whose rows start at different
+        times)."""
+        if check and self.filled + 1 >= self.smax:
             raise RuntimeError("KV cache full")
         if self.graph is not None:
             self.graph.replay()

@@ -1,4 +1,5 @@
-"""RCCL all-reduce bus-bandwidth sweep (N3 in SURVEY.md §2.5).
+"""RCCL all-reduce bus-bandwidth sweep (the reference's "142 -> 228 GB/s"
+all-reduce metric, docs/PRD.md:119-124, measured here over xGMI).
 
 Two drivers for the same measurement:
   * ``native``: one process, ncclCommInitAll over the visible GPUs

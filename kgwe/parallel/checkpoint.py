@@ -1,5 +1,4 @@
-"""Sharded checkpoint / resume for the data-parallel trainer (SURVEY.md §5.4:
-the reference keeps all state in process memory; its example mounts a
+"""Sharded checkpoint / resume for the data-parallel trainer (the reference keeps all state in process memory; its example mounts a
 checkpoint PVC for the user job, examples/distributed-training.yaml:80-90).
 
 What a rescheduled workload (controller ``spec.recovery``) resumes from:

@@ -1,7 +1,7 @@
 """Config system: defaults <- YAML file <- environment <- --set flags.
 
-Reference: Go `Default*Config()` constructors mirrored by Helm values
-(SURVEY.md §5.6), many of whose keys were never read.  Here every binary
+Reference: Go `Default*Config()` constructors mirrored by Helm values, many
+of whose keys were never read.  Here every binary
 declares its full default tree; a key that is not in the tree is REJECTED
 (no silently ignored settings), and values are coerced to the default's type.
 

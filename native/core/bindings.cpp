@@ -45,10 +45,12 @@ PlatformConfig config_from_json(const std::string& s) {
   c.enforce_budgets = j.get("enforceBudgets").as_bool(true);
   c.master_port = static_cast<int>(j.get("masterPort").as_int(29500));
   c.gpu_resource = j.get("gpuResource").str("amd.com/gpu");
+  c.share_socket_dir = j.get("shareSocketDir").str(c.share_socket_dir);
   c.consolidate.below = j.get("partitionConsolidateBelow").as_number(c.consolidate.below);
   c.consolidate.after_s = j.get("partitionConsolidateAfterSeconds").as_number(c.consolidate.after_s);
   c.consolidate.cooldown_s = j.get("migrationCooldownSeconds").as_number(c.consolidate.cooldown_s);
   c.sched.max_share_clients = static_cast<int>(sc.get("maxShareClients").as_int(c.sched.max_share_clients));
+  c.sched.max_group_clients = static_cast<int>(sc.get("maxGroupClients").as_int(c.sched.max_group_clients));
   c.sched.preemption_candidate_nodes =
       static_cast<int>(sc.get("preemptionCandidateNodes").as_int(c.sched.preemption_candidate_nodes));
   c.sched.preemption_wait_window_s = sc.get("preemptionWaitWindowSeconds").as_number(c.sched.preemption_wait_window_s);

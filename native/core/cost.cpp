@@ -705,7 +705,7 @@ void CostEngine::replay() {
     if (line.empty()) continue;
     try {
       Json j = Json::parse(line);
-      const std::string ev = j.has("ev") ? j.get("ev").str() : "final";  // round-1 lines: finals
+      const std::string ev = j.has("ev") ? j.get("ev").str() : "final";  // lines without an event tag are finals (older journals)
       UsageRecord r = usage_from_json(j.has("record") ? j.get("record") : j);
       if (ev == "final") {
         r.finalized = true;

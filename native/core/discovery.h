@@ -6,7 +6,7 @@
 // MI355X-native redesign:
 //   * the new snapshot is built OFF-lock and published with an atomic
 //     shared_ptr swap, so schedulers never block on a refresh (the reference
-//     held the write lock for the whole refresh, §3b of SURVEY.md);
+//     held the write lock for the whole refresh, discovery.go:290-319);
 //   * every node has its own HAL (real amd-smi agent or fixture), instead of
 //     querying one local NVML handle for every node (discovery.go:323,334);
 //   * node agents may also PUSH their topology (upsert_node), which is how a

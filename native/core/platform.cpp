@@ -90,6 +90,7 @@ WorkloadRequest workload_from_pod(const Json& pod, const std::string& gpu_resour
       w.gpu_count = 1;
       w.share_cu_percent = std::atof(ann.get("kgwe.amd.com/cu-percent").str("0").c_str());
       w.share_memory_gb = std::atof(ann.get("kgwe.amd.com/memory-gb").str("0").c_str());
+      w.share_group = ann.get("kgwe.amd.com/share-group").str();
       if (!ann.has("kgwe.amd.com/workload-type")) w.type = WorkloadType::Inference;
     }
   }
@@ -502,6 +503,17 @@ std::string Platform::placement_json(const WorkloadRequest& w, const Decision& d
       for (const auto& kv : share_env(d.sharing, g.index, d.cu_begin, d.cu_end, d.share_memory_gb,
                                       g.memory_total_gb))
         env[kv.first] = kv.second;
+    if (!d.share_group.empty()) {
+      // One serving process per (GPU, group): the leader listens on a socket
+      // in the node's share directory, the members connect to it.
+      env["KGWE_SHARE_GROUP"] = d.share_group;
+      env["KGWE_SHARE_ROLE"] = d.share_leader ? "leader" : "member";
+      env["KGWE_SHARE_LEADER"] = d.share_leader_uid;
+      std::string file = d.shared_gpu + "-" + d.share_group;
+      for (auto& c : file)
+        if (!(std::isalnum(static_cast<unsigned char>(c)) || c == '-' || c == '_' || c == '.')) c = '_';
+      env["KGWE_BATCH_ENDPOINT"] = "unix:" + cfg_.share_socket_dir + "/" + file + ".sock";
+    }
   }
   pl["env"] = env;
   pl["workload"] = to_json(w);
@@ -651,6 +663,8 @@ std::string Platform::schedule(const std::string& workload_json) {
 std::string Platform::release(const std::string& uid, double now_s) {
   Allocation a;
   const bool had = sched_->allocation(uid, &a);
+  bool was_leader = false;
+  const std::vector<std::string> group_peers = sched_->share_group_peers(uid, &was_leader);
   bool ok = sched_->release(uid);
   {
     std::lock_guard<std::mutex> lk(pods_mu_);
@@ -659,6 +673,14 @@ std::string Platform::release(const std::string& uid, double now_s) {
   UsageRecord r;
   Json out = Json::object();
   out["released"] = ok;
+  if (ok && was_leader && !group_peers.empty()) {
+    // The group's serving process went with its leader: the members have
+    // nothing to connect to.  The controller evicts them; rescheduled, the
+    // first becomes the new leader.
+    Json oj = Json::array();
+    for (const auto& p : group_peers) oj.push_back(p);
+    out["orphaned_share_members"] = oj;
+  }
   {
     // A preemption victim whose gang has members on other nodes: they are
     // the controller's to evict (see preempt()).

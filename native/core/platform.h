@@ -4,7 +4,7 @@
 // Reference: the extender contract exists only as configuration
 // (deploy/helm/kgwe/templates/scheduler-configmap.yaml:61-79: verbs filter /
 // prioritize / bind, weight 100, nodeCacheCapable false, managed resources);
-// no server, no glue and no constructor calls exist (SURVEY.md §0).  Here:
+// no server, no glue and no constructor calls exist.  Here:
 //   filter      ExtenderArgs          -> ExtenderFilterResult
 //                 (+ budget admission, + partition auto-provisioning — the
 //                  designed PreBind "KGWEMIGProvisioning" plugin)
@@ -39,6 +39,9 @@ struct PlatformConfig {
   bool enforce_budgets = true;
   int master_port = 29500;
   std::string gpu_resource = "amd.com/gpu";
+  // Node directory (a hostPath shared by the share pods of a node) where a
+  // share group's leader puts its serving socket.
+  std::string share_socket_dir = "/run/kgwe/share";
   ConsolidationPolicy consolidate;
 };
 
@@ -48,7 +51,7 @@ struct PlatformConfig {
 // spec.priority / nodeSelector / tolerations / nodeAffinity.
 WorkloadRequest workload_from_pod(const Json& pod, const std::string& gpu_resource = "amd.com/gpu");
 
-// RCCL-over-xGMI rank environment for a placement (SURVEY.md §5.8 / N5).
+// RCCL-over-xGMI rank environment for a placement.
 std::map<std::string, std::string> rccl_env(const WorkloadRequest& w, const Decision& d,
                                             const NodeTopology& node, int master_port,
                                             const std::string& master_addr = "");

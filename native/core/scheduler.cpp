@@ -181,6 +181,7 @@ WorkloadRequest workload_from_json(const Json& in) {
     if (w.sharing == SharingMethod::Partition) w.sharing = SharingMethod::None;  // use `partition`
     w.share_cu_percent = share.get("cuPercent").as_number(0.0);
     w.share_memory_gb = share.get("memoryGB").as_number(0.0);
+    w.share_group = share.get("group").str();
     if (w.sharing != SharingMethod::None) w.gpu_count = 1;
   }
   const Json& mig = req.get("mig");  // legacy MIG field: map profile size to a mode
@@ -257,6 +258,7 @@ Json to_json(const WorkloadRequest& w) {
     j["sharing"] = to_string(w.sharing);
     j["share_cu_percent"] = w.share_cu_percent;
     j["share_memory_gb"] = w.share_memory_gb;
+    if (!w.share_group.empty()) j["share_group"] = w.share_group;
   }
   return j;
 }
@@ -279,6 +281,11 @@ Json to_json(const Decision& d) {
     j["cu_begin"] = d.cu_begin;
     j["cu_end"] = d.cu_end;
     j["share_memory_gb"] = d.share_memory_gb;
+    if (!d.share_group.empty()) {
+      j["share_group"] = d.share_group;
+      j["share_leader"] = d.share_leader;
+      j["share_leader_uid"] = d.share_leader_uid;
+    }
   }
   j["score"] = d.score;
   j["bandwidth_gbps"] = d.bandwidth_gbps;
@@ -319,6 +326,11 @@ Json to_json(const Allocation& a) {
     j["cu_begin"] = a.cu_begin;
     j["cu_end"] = a.cu_end;
     j["share_memory_gb"] = a.share_memory_gb;
+    if (!a.share_group.empty()) {
+      j["share_group"] = a.share_group;
+      j["share_leader"] = a.share_leader;
+      j["share_leader_uid"] = a.share_leader_uid;
+    }
   }
   j["type"] = to_string(a.type);
   j["priority"] = a.priority;
@@ -350,6 +362,9 @@ Allocation allocation_from_json(const Json& j) {
   a.cu_begin = static_cast<int>(j.get("cu_begin").as_int(0));
   a.cu_end = static_cast<int>(j.get("cu_end").as_int(0));
   a.share_memory_gb = j.get("share_memory_gb").as_number(0.0);
+  a.share_group = j.get("share_group").str();
+  a.share_leader = j.get("share_leader").as_bool(false);
+  a.share_leader_uid = j.get("share_leader_uid").str();
   a.type = workload_type_from(j.get("type").str("Training"));
   a.priority = j.get("priority").as_int(0);
   a.preemptible = j.get("preemptible").as_bool(true);
@@ -990,6 +1005,31 @@ bool Scheduler::share_fits(const GpuDevice& g, const WorkloadRequest& w, int* cu
       if (it != allocs_.end()) clients.push_back(&it->second);
     }
   }
+  if (!w.share_group.empty()) {
+    // Join the group's share on this GPU: its CU range and HBM cap, no new ones.
+    int members = 0;
+    const Allocation* lead = nullptr;
+    for (auto* c : clients)
+      if (c->share_group == w.share_group) {
+        ++members;
+        if (c->share_leader || !lead) lead = c;
+      }
+    if (lead) {
+      if (!lead->share_leader) return false;  // the group's server is gone: its orphans are being evicted
+      if (members >= cfg_.max_group_clients) return false;
+      *cu_begin = lead->cu_begin;
+      *cu_end = lead->cu_end;
+      return true;
+    }
+  }
+  // A group counts as one client of the GPU.
+  {
+    std::set<std::string> groups;
+    std::vector<const Allocation*> distinct;
+    for (auto* c : clients)
+      if (c->share_group.empty() || groups.insert(c->share_group).second) distinct.push_back(c);
+    clients.swap(distinct);  // (members carry no HBM cap of their own: the leader's covers the group)
+  }
   double mem = 0.0;
   for (auto* c : clients) mem += c->share_memory_gb;
   const double cap = g.memory_total_gb > 0 ? g.memory_total_gb : 288.0;
@@ -1052,6 +1092,11 @@ bool Scheduler::pick_share(const NodeTopology& n, const WorkloadRequest& w, Node
     auto sh = shared_.find(g.uuid);
     const int clients = sh == shared_.end() ? 0 : static_cast<int>(sh->second.clients.size());
     std::tuple<int, int, int> key{clients == 0 ? 1 : 0, -clients, g.index};
+    if (!w.share_group.empty() && sh != shared_.end())
+      for (const auto& uid : sh->second.clients) {
+        auto it = allocs_.find(uid);
+        if (it != allocs_.end() && it->second.share_group == w.share_group) std::get<0>(key) = -1;  // its group is here
+      }
     if (!best || key < bkey) {
       best = &g;
       bkey = key;
@@ -1069,6 +1114,7 @@ bool Scheduler::pick_share(const NodeTopology& n, const WorkloadRequest& w, Node
 NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w) const {
   NodeScore s;
   s.node = n.name;
+  int group_bonus = 0;
   if (w.sharing != SharingMethod::None) {
     if (!pick_share(n, w, &s)) return s;
     auto sh = shared_.find(s.shared_gpu);
@@ -1076,6 +1122,14 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
     s.topology = 100;
     s.resource = clients > 0 ? 100 : 50;  // packing onto already-shared GPUs
     s.balance = balance_score(n, clients > 0 ? 0 : 1);
+    if (!w.share_group.empty() && sh != shared_.end())
+      for (const auto& uid : sh->second.clients) {
+        auto it = allocs_.find(uid);
+        if (it != allocs_.end() && it->second.share_group == w.share_group && group_bonus == 0) {
+          group_bonus = 30;  // join the group's server rather than start a second one elsewhere
+          s.reasons.push_back("share group " + w.share_group + " is served on this GPU");
+        }
+      }
   } else if (w.partition) {
     std::vector<std::string> gpu_of;
     auto parts = free_partitions(n, w, &gpu_of);
@@ -1113,6 +1167,7 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
   }
   s.total = (s.topology * cfg_.topology_weight + s.resource * cfg_.resource_weight +
              s.balance * cfg_.balance_weight) / 100;
+  s.total += group_bonus;
   if (std::find(w.preferred_nodes.begin(), w.preferred_nodes.end(), n.name) != w.preferred_nodes.end()) {
     s.total += 10;
     s.reasons.push_back("workload optimizer prefers this node");
@@ -1179,6 +1234,7 @@ uint64_t Scheduler::request_signature(const WorkloadRequest& w) {
   num(static_cast<int>(w.sharing));
   num(w.share_cu_percent);
   num(w.share_memory_gb);
+  str(w.share_group);
   for (const auto& kv : w.node_selector) {
     str(kv.first);
     str(kv.second);
@@ -1476,6 +1532,21 @@ bool Scheduler::reserve_locked(const WorkloadRequest& w, const NodeScore& s, boo
     a.cu_begin = b;
     a.cu_end = e;
     a.share_memory_gb = w.share_memory_gb;
+    a.share_group = w.share_group;
+    if (!w.share_group.empty()) {
+      a.share_leader = true;
+      a.share_leader_uid = w.uid;
+      auto cur = shared_.find(s.shared_gpu);
+      if (cur != shared_.end())
+        for (const auto& uid : cur->second.clients) {
+          auto it = allocs_.find(uid);
+          if (it != allocs_.end() && it->second.share_group == w.share_group && it->second.share_leader) {
+            a.share_leader = false;  // a member: the leader's range and cap cover it
+            a.share_leader_uid = uid;
+            a.share_memory_gb = 0.0;
+          }
+        }
+    }
     a.type = w.type;
     a.priority = w.priority;
     a.preemptible = w.preemptible;
@@ -1586,6 +1657,9 @@ static Decision decision_from(const Allocation& a, int score, const std::string&
   d.cu_begin = a.cu_begin;
   d.cu_end = a.cu_end;
   d.share_memory_gb = a.share_memory_gb;
+  d.share_group = a.share_group;
+  d.share_leader = a.share_leader;
+  d.share_leader_uid = a.share_leader_uid;
   d.score = score;
   d.bandwidth_gbps = a.bandwidth_gbps;
   return d;
@@ -2429,6 +2503,22 @@ Decision Scheduler::reserve_share(const WorkloadRequest& w, const std::string& n
   lk.unlock();
   emit({SchedEventType::Scheduled, w.uid, node, "share", now_ns()});
   return d;
+}
+
+std::vector<std::string> Scheduler::share_group_peers(const std::string& uid, bool* leader) const {
+  std::vector<std::string> out;
+  *leader = false;
+  std::shared_lock<RwLock> lk(mu_);
+  auto it = allocs_.find(uid);
+  if (it == allocs_.end() || it->second.share_group.empty()) return out;
+  *leader = it->second.share_leader;
+  auto sh = shared_.find(it->second.shared_gpu);
+  if (sh == shared_.end()) return out;
+  for (const auto& c : sh->second.clients) {
+    auto a = allocs_.find(c);
+    if (c != uid && a != allocs_.end() && a->second.share_group == it->second.share_group) out.push_back(c);
+  }
+  return out;
 }
 
 int Scheduler::share_clients(const std::string& gpu_uuid) const {

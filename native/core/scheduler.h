@@ -17,7 +17,7 @@
 //     anti-affinity, minMemoryGB, minBandwidthGBps, arch (k GPUs of it, not
 //     "any"), xGMIRequired as a hard constraint;
 //   * events go to a bounded ring (never blocks), metrics are lock-consistent.
-// MI355X-first scoring (§5.8 of SURVEY.md): an 8xMI355X node is an all-to-all
+// MI355X-first scoring: an 8xMI355X node is an all-to-all
 // xGMI mesh, so every k-subset is pairwise equivalent under the reference's
 // clique search; the native scorer ranks groups by MEASURED link bandwidth
 // (degraded/down links), NUMA/socket compactness and fragmentation (largest
@@ -111,6 +111,10 @@ struct WorkloadRequest {
   SharingMethod sharing = SharingMethod::None;
   double share_cu_percent = 0.0;   // 0 = policy default
   double share_memory_gb = 0.0;    // 0 = no cap
+  // Clients of one share group (same model, one serving process) hold ONE CU
+  // range and ONE HBM cap on a GPU between them: the first is the group's
+  // leader (runs the server), the rest are members that connect to it.
+  std::string share_group;
   double max_latency_ms = 0.0;
   std::vector<std::string> preferred_nodes;  // optimizer hint (+10 bonus)
   // How long the workload is expected to hold its GPUs (spec
@@ -144,6 +148,9 @@ struct Allocation {
   std::string shared_gpu;
   int cu_begin = 0, cu_end = 0;  // [begin, end) of the GPU's CUs (CoLocate)
   double share_memory_gb = 0.0;
+  std::string share_group;       // "" = a share of its own
+  bool share_leader = false;     // first client of its group on the GPU (holds the range and the cap)
+  std::string share_leader_uid;  // the group's leader (itself for the leader)
   WorkloadType type = WorkloadType::Training;
   int64_t priority = 0;
   bool preemptible = true;
@@ -162,6 +169,8 @@ struct Decision {
   SharingMethod sharing = SharingMethod::None;
   int cu_begin = 0, cu_end = 0;
   double share_memory_gb = 0.0;
+  std::string share_group, share_leader_uid;  // group shares: who runs the group's server
+  bool share_leader = false;
   int score = 0;
   double bandwidth_gbps = 0.0;
   double latency_ms = 0.0;
@@ -190,6 +199,7 @@ struct SchedulerConfig {
   int max_share_clients = 8;          // co-located clients per GPU
   double default_cu_percent = 12.5;   // one XCD (32 of 256 CUs)
   int max_timeslice_replicas = 4;
+  int max_group_clients = 32;         // members of one share group on a GPU
   // Preemption policy.  Victims are planned exactly only on the K nodes a
   // cheap per-node estimate ranks best; an allocation expected to finish
   // within the wait window is not a victim, and a request whose room such
@@ -283,6 +293,9 @@ class Scheduler {
   NodeSummary node_summary(const NodeTopology& n) const;
   // Share clients currently on a GPU (CoLocate / TimeSlice).
   int share_clients(const std::string& gpu_uuid) const;
+  // Members of `uid`'s share group left on its GPU (uid itself excluded), and
+  // whether uid is the group's leader: what a release has to tell the controller.
+  std::vector<std::string> share_group_peers(const std::string& uid, bool* leader) const;
   // Partition-switch fence: atomically (under the ledger lock) check that no
   // whole-GPU or slice reservation holds `gpu_uuid` and bar new ones until
   // unfence_gpu.  Closes the window between the controller's idle check and

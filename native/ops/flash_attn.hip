@@ -225,7 +225,7 @@ __device__ __forceinline__ u16x4 tr_read(const bf16_t* lds_base, int byte_off) {
 // at B=4, S=4096 causal the forward goes 0.672-0.684 -> 0.650-0.654 ms; the
 // numerics cases (growing max, a x6 max jump mid-sweep) stay within one bf16
 // ulp of the fp32 reference (tools/fa_fwd_err.py: max 1.56e-2 at |O| ~ 2-4).
-// T = 8 had failed the max-jump case at 2 ulps (round-2 session 1).
+// T = 8 had failed the max-jump case at 2 ulps.
 #ifndef FA_DEFER_T
 #define FA_DEFER_T 4.f
 #endif
@@ -249,7 +249,7 @@ static_assert(FNW * QPW <= 8 && 16 % FNW == 0, "at most 256 query rows, 16 stagi
 // after them, so one barrier per tile separates the phases.
 // Default geometry, measured with tools/fa_variants.hip (B=2, S=4096):
 // 8 waves x 1 sub-block = 256 rows per workgroup, one 512-thread workgroup
-// per CU (67 KB LDS, <= 256 VGPRs per wave, two waves per SIMD).  In round 1
+// per CU (67 KB LDS, <= 256 VGPRs per wave, two waves per SIMD).  Earlier
 // the 4-wave / two-workgroups-per-CU form won (641 vs 622 TF/s,
 // profiles/r01_attn_counters/NOTES.md: barrier coupling of the two waves on
 // a SIMD); after the VALU trims, longest-first dispatch and 16-B epilogue

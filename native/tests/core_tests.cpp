@@ -1,5 +1,5 @@
-// Native unit + concurrency tests for the C++ platform core (SURVEY.md §4
-// test plan item 1, §5.2 race detection).  Plain asserts, no framework; one
+// Native unit + concurrency tests for the C++ platform core (the reference's
+// `go test -race` role: Makefile:79-85).  Plain asserts, no framework; one
 // binary per build flavour (plain, -fsanitize=thread, -fsanitize=address,
 // undefined), driven by tests/test_native_core.py.
 //

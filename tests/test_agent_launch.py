@@ -2,6 +2,7 @@
 launcher, and the GPU-side probes / RCCL sweep (gpu-marked)."""
 import http.client
 import json
+import os
 
 import pytest
 
@@ -260,3 +261,28 @@ def test_advertised_endpoint_must_be_an_address_of_the_node_object(tmp_path):
             ext.stop()
     finally:
         api.stop()
+
+
+def test_launcher_installs_the_hbm_cap_hook_for_shares_only(tmp_path):
+    """A placement with an HBM cap makes every Python process of the workload
+    load kgwe/_sitehook first; the hook arms itself on `import torch` and does
+    nothing before.  No cap in the placement: PYTHONPATH is left alone."""
+    import subprocess
+    import sys
+
+    from kgwe import launch
+
+    env = launch.enforce_share_limits({"KGWE_GPU_MEMORY_FRACTION": "0.25", "PYTHONPATH": "/x"})
+    assert env["PYTHONPATH"].split(os.pathsep) == [launch.SITEHOOK, "/x"]
+    assert "PYTHONPATH" not in launch.enforce_share_limits({"KGWE_GPU_MEMORY_FRACTION": "0"})
+    assert "PYTHONPATH" not in launch.enforce_share_limits({})
+    ann = tmp_path / "annotations"
+    ann.write_text('kgwe.amd.com/rccl-env=' + json.dumps(json.dumps({"KGWE_GPU_MEMORY_FRACTION": "0.25"})) + "\n")
+    code = ("import os, sys; print('pre', os.environ.get('KGWE_GPU_MEMORY_CAP_INSTALLED'), 'torch' in sys.modules); "
+            "import torch; print('post', os.environ.get('KGWE_GPU_MEMORY_CAP_INSTALLED'))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "kgwe.launch", "--", sys.executable, "-c", code], cwd=root,
+                       env=dict(os.environ, KGWE_ANNOTATIONS_FILE=str(ann)), capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-800:]
+    assert "pre None False" in r.stdout and "post 1" in r.stdout

@@ -1,5 +1,5 @@
-"""Real amd-smi through the C++ AmdSmiHal on an MI355X (SURVEY.md §4 item 4:
-real discovery + telemetry sampler): device identity, HBM size, partition
+"""Real amd-smi through the C++ AmdSmiHal on an MI355X (real
+discovery + telemetry sampler): device identity, HBM size, partition
 modes, RAS / xGMI / throttle health signals and the health policy, the
 scheduler running on the discovered node, and gfx_activity under load."""
 from __future__ import annotations

@@ -1,4 +1,4 @@
-"""Sharded checkpoint / resume of the data-parallel trainer (SURVEY.md §5.4),
+"""Sharded checkpoint / resume of the data-parallel trainer,
 gloo on CPU: an interrupted-and-resumed run matches an uninterrupted one
 bit for bit, and a checkpoint written by 2 ranks resumes on 1 (elastic)."""
 from __future__ import annotations
@@ -120,7 +120,7 @@ def test_gpu_checkpoint_side_stream_roundtrip(tmp_path):
 
 @pytest.mark.gpu
 def test_gpu_checkpoint_mid_training_holds_one_step(tmp_path):
-    """a checkpoint saved while training continues must hold
+    """A checkpoint saved while training continues must hold
     exactly the state of its step.  The D2H snapshot runs on a side stream
     and the next steps' AdamW must wait for it (``dp.fence_writes``); the
     step-2 file is compared with a device-side clone taken on the compute

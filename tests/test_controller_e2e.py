@@ -295,7 +295,7 @@ def _status(kube, ns, name):
 
 
 def test_node_loss_reschedules_workload(cluster):
-    """the reference evicts a deleted node from its cache and
+    """The reference evicts a deleted node from its cache and
     leaves the allocations on it stale.  Here the workload is evicted and,
     per spec.recovery, rescheduled onto the surviving node."""
     api, kube, plat, ext, rec = cluster
@@ -380,7 +380,7 @@ def _cluster(sets: list[str], nodes: int = 2):
 def test_optimizer_loop_recommends_cpx_from_live_telemetry():
     """The running controller feeds per-allocation telemetry to the optimizer,
     writes status.recommendation (rightsizing) and trains the online model on
-    completions — no hand-fed optimizer object (VERDICT r1 item 7)."""
+    completions — no hand-fed optimizer object."""
     api, kube, plat, ext, rec, stop = _cluster(["optimizer.recommendEverySeconds=0.5"])
     try:
         kube.create_cr(gw("serve", count=0, workloadType="Inference", framework="PyTorch",

@@ -1,4 +1,4 @@
-"""SURVEY.md §7.4 minimum end-to-end slice on one MI355X: a GPUWorkload is
+"""Minimum end-to-end slice on one MI355X: a GPUWorkload is
 placed by the C++ scheduler (xGMI-aware, RCCL env rendered), the placement is
 written as the downward-API annotations file, ``kgwe.launch`` turns it into
 the process environment and execs the trainer, which trains on the GPU over

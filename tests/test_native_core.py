@@ -1,5 +1,5 @@
 """Standalone C++ tests of the platform core (native/tests/core_tests.cpp):
-plain, ThreadSanitizer and ASan+UBSan builds (SURVEY.md §4 item 1, §5.2).
+plain, ThreadSanitizer and ASan+UBSan builds.
 
 The stress case runs 8 scheduler threads (schedule / extender filter+bind /
 partition auto-provision / release) against topology refresh, the

@@ -17,7 +17,7 @@ def dp(t, util, mem_gb, total_gb=288):
 
 def test_reference_table_parity():
     opt = WorkloadOptimizer(sizing="reference", learn=False)
-    # Verified reference outputs: 7B -> 2 GPUs, 13B -> 4, 70B -> 16.
+    # Outputs of the reference's predictor (workload_optimizer.py:275-285, run with numpy 2.2): 7B -> 2 GPUs, 13B -> 4, 70B -> 16.
     assert opt.predict_resources("a", {"model_params_billions": 7}).recommended_gpus == 2
     assert opt.predict_resources("a", {"model_params_billions": 13}).recommended_gpus == 4
     assert opt.predict_resources("a", {"model_params_billions": 70}).recommended_gpus == 16

@@ -1,6 +1,6 @@
 """Scheduler core (C++) — placement, filters, preemption, gangs, ledger safety.
 
-Maps to SURVEY.md §4 test plan items 1/3: scorers against the reference
+Covers: scorers against the reference
 formulas (compat mode), every filter constraint, ledger atomicity under
 concurrency, bounded priority-aware preemption, gang all-or-nothing, and a p99
 that comes from the histogram (not a running max).
@@ -245,7 +245,7 @@ def test_topology_hints(plat):
     ({"cper_corrected": 3}, "Healthy", None),
 ])
 def test_health_policy_from_ras_signals(plat, signals, status, reason):
-    """Fault injection through the fake amd-smi (SURVEY.md §5.3): raw RAS /
+    """Fault injection through the fake amd-smi: raw RAS /
     xGMI / throttle signals -> the shared health policy -> schedulability."""
     gpu = "GPU-n0-02"
     plat.fake_set_health_signals("n0", gpu, signals)

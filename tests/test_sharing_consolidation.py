@@ -342,3 +342,78 @@ def test_share_placement_counts_hbm_the_device_reports_in_use():
     assert not p.schedule(share_wl("big", mem=30.0))["ok"]
     d = p.schedule(share_wl("small", mem=10.0))
     assert d["ok"] and d["shared_gpu"] == busy
+
+
+# --- share groups: same-model clients behind one serving process ------------------------------
+
+def group_wl(uid, group, cu=50.0, mem=40.0):
+    w = share_wl(uid, cu=cu, mem=mem)
+    w["spec"]["gpuRequirements"]["sharing"]["group"] = group
+    return w
+
+
+def test_share_group_members_ride_on_the_leaders_range_and_cap():
+    p = Platform({"enforceBudgets": False, "shareSocketDir": "/run/kgwe/share"})
+    for n in ("a", "b"):
+        p.add_fake_node(make_fixture(n, 8, 2))
+    lead = p.schedule(group_wl("m0", "llama-1b"))
+    assert lead["ok"] and lead["share_leader"] and lead["share_leader_uid"] == "m0"
+    assert (lead["cu_begin"], lead["cu_end"]) == (0, 128) and lead["share_memory_gb"] == 40.0
+    env = lead["env"]
+    assert env["KGWE_SHARE_ROLE"] == "leader" and env["KGWE_SHARE_GROUP"] == "llama-1b"
+    sock = env["KGWE_BATCH_ENDPOINT"]
+    assert sock == f"unix:/run/kgwe/share/{lead['shared_gpu']}-llama-1b.sock"
+    members = [p.schedule(group_wl(f"m{k}", "llama-1b")) for k in range(1, 8)]
+    for d in members:
+        # same GPU, same CU range, no HBM of their own, and the leader's socket
+        assert d["ok"] and d["shared_gpu"] == lead["shared_gpu"] and not d["share_leader"]
+        assert (d["cu_begin"], d["cu_end"]) == (0, 128) and d["share_memory_gb"] == 0.0
+        assert d["env"]["KGWE_SHARE_ROLE"] == "member" and d["env"]["KGWE_BATCH_ENDPOINT"] == sock
+        assert d["env"]["KGWE_SHARE_LEADER"] == "m0" and "KGWE_GPU_MEMORY_FRACTION" not in d["env"]
+    # the group is ONE client of the GPU: the other half of the CUs still takes an ordinary share
+    other = p.schedule(share_wl("solo", cu=50.0, mem=100.0))
+    assert other["ok"] and other["shared_gpu"] == lead["shared_gpu"]
+    assert (other["cu_begin"], other["cu_end"]) == (128, 256)
+    # another group gets a range (and a leader) of its own
+    d = p.schedule(group_wl("x0", "mistral", cu=12.5, mem=20.0))
+    assert d["ok"] and d["share_leader"] and d["shared_gpu"] != lead["shared_gpu"]
+    m = p.scheduler_metrics()
+    assert m["share_clients"] == 10
+
+
+def test_share_group_size_is_bounded_and_a_full_group_starts_a_second_server():
+    p = Platform({"enforceBudgets": False, "scheduler": {"maxGroupClients": 3}})
+    p.add_fake_node(make_fixture("a", 2, 1))
+    ds = [p.schedule(group_wl(f"c{k}", "g", cu=25.0, mem=10.0)) for k in range(5)]
+    assert all(d["ok"] for d in ds)
+    assert [d["share_leader"] for d in ds] == [True, False, False, True, False]
+    assert ds[3]["share_leader_uid"] == "c3" and ds[4]["share_leader_uid"] == "c3"
+
+
+def test_releasing_a_group_leader_names_its_orphans_and_blocks_new_joiners():
+    p = Platform({"enforceBudgets": False})
+    p.add_fake_node(make_fixture("a", 1, 1))
+    for k in range(3):
+        assert p.schedule(group_wl(f"c{k}", "g", cu=100.0, mem=10.0))["ok"]
+    assert "orphaned_share_members" not in p.release("c2")          # a member leaves: nothing to do
+    rel = p.release("c0")
+    assert rel["orphaned_share_members"] == ["c1"]
+    # nobody may join a group whose server is gone, and its CUs are still held by the orphan
+    assert not p.schedule(group_wl("late", "g", cu=100.0, mem=10.0))["ok"]
+    assert p.release("c1")["released"]
+    d = p.schedule(group_wl("late", "g", cu=100.0, mem=10.0))
+    assert d["ok"] and d["share_leader"]
+
+
+def test_share_group_survives_a_ledger_rebuild():
+    p = Platform({"enforceBudgets": False})
+    p.add_fake_node(make_fixture("a", 1, 1))
+    for k in range(2):
+        assert p.schedule(group_wl(f"c{k}", "g", cu=50.0, mem=10.0))["ok"]
+    saved = p.allocations()
+    q = Platform({"enforceBudgets": False})
+    q.add_fake_node(make_fixture("a", 1, 1))
+    for a in saved:
+        assert q.restore_allocation(a)
+    d = q.schedule(group_wl("c2", "g", cu=50.0, mem=10.0))
+    assert d["ok"] and not d["share_leader"] and d["share_leader_uid"] == "c0"

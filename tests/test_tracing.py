@@ -1,5 +1,5 @@
-"""OTLP/HTTP JSON span export of the extender's scheduling phases (SURVEY.md
-§5.1, reference README.md:43 / docs/PRD.md:440: OpenTelemetry claimed, absent).
+"""OTLP/HTTP JSON span export of the extender's scheduling phases (reference
+README.md:43 / docs/PRD.md:440: OpenTelemetry claimed, absent).
 A stdlib HTTP server stands in for an OpenTelemetry Collector."""
 from __future__ import annotations
 
