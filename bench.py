@@ -86,8 +86,12 @@ def parse(argv=None):
                          "optimizer/gradients (kgwe.parallel.zero, default); fsdp: PyTorch FSDP2")
     ap.add_argument("--fsdp-row", default="auto", choices=["auto", "on", "off"],
                     help="also time an FSDP2 row after the headline (auto: when N > 1)")
-    ap.add_argument("--reduce-dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="gradient reduce-scatter dtype of the sharded-DP path at N > 1")
+    ap.add_argument("--reduce-dtype", default="bf16", choices=["fp32", "bf16"],
+                    help="gradient reduce-scatter dtype of the sharded-DP path at N > 1.  bf16 (default): "
+                         "half the bytes over xGMI, and the weight-gradient GEMMs write straight into the "
+                         "reduce-scatter buckets (no gradient copy); against fp32 it moves the weights by "
+                         "no more than the bf16 rounding of the gradients themselves does "
+                         "(tests/test_parallel_cpu.py, worlds 4 and 8)")
     ap.add_argument("--reduce-row", default="auto", choices=["auto", "on", "off"],
                     help="also time the sharded-DP path with the OTHER reduce dtype for a few "
                          "steps (auto: at N > 1 on RCCL) — what halving the reduce-scatter "

@@ -32,6 +32,8 @@ def lib():
         L.kgwe_probe_p2p_all.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_double)]
         L.kgwe_probe_p2p_all.restype = ctypes.c_int
+        L.kgwe_probe_gate_selftest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.kgwe_probe_gate_selftest.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -129,3 +131,12 @@ def main(argv=None) -> int:
 
 if __name__ == "__main__":
     raise SystemExit(main())
+
+
+def gate_selftest(device: int = 0, raise_flag: bool = True, limit_us: int = 2000) -> int:
+    """The all-links probe's start gate on one device: 1 = the kernel saw the
+    host's flag, 0 = its bounded wait ran out (the flag was never raised)."""
+    rc = lib().kgwe_probe_gate_selftest(device, 1 if raise_flag else 0, limit_us)
+    if rc < 0:
+        raise RuntimeError(f"kgwe_probe_gate_selftest failed rc={rc}")
+    return rc

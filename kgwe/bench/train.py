@@ -42,7 +42,7 @@ class TrainConfig:
     ckpt_every: int = 0          # steps between checkpoints (0: only at the end of run())
     # gradient reduce-scatter dtype of the sharded-DP path at world > 1: fp32
     # (exact sums) or bf16 (half the xGMI bytes per step)
-    reduce_dtype: torch.dtype = torch.float32
+    reduce_dtype: torch.dtype = torch.bfloat16  # gradient reduce-scatter at world > 1 (see kgwe.parallel.zero)
 
 
 _T0 = time.perf_counter()

@@ -241,6 +241,23 @@ def _wgrad_mode() -> str:
     return mode
 
 
+def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """dW[N, K] = dY[T, N]^T X[T, K] by the fastest route for the shape; with
+    ``out`` (contiguous, dY's dtype) the GEMM writes there — the data-parallel
+    wrapper passes the parameter's slice of its gradient bucket, so no copy of
+    the gradient is ever made."""
+    N, K = dy2.shape[1], x2.shape[1]
+    mode = _wgrad_mode()
+    if (mode != "library" and (N < K or mode == "kernel") and wgrad_supported(dy2, x2)
+            and (out is None or out.data_ptr() % 8 == 0)):
+        return wgrad(dy2, x2, out=out)
+    if x2.shape[0] % 8 or N % 8 or K % 8 or not x2.is_contiguous():
+        return torch.mm(dy2.t(), x2, out=out)
+    if N >= K:
+        return torch.mm(dy2.t(), transpose(x2).t(), out=out)   # "tt"
+    return torch.mm(transpose(dy2), x2, out=out)               # "nn"
+
+
 class _Linear(torch.autograd.Function):
     """y = x W^T.  Forward is the plain library GEMM ("nt"); the input
     gradient uses the weight's persistent transposed copy when one exists
@@ -255,7 +272,11 @@ class _Linear(torch.autograd.Function):
     projection) the hand-written MFMA kernel of kgwe.ops.gemm takes both
     operands as stored and is the faster of the two (1.70 vs 1.82 ms at
     [4096, 14336] over 16,384 tokens); ``KGWE_WGRAD=kernel`` uses it for every
-    shape it supports, ``KGWE_WGRAD=library`` never."""
+    shape it supports, ``KGWE_WGRAD=library`` never.
+
+    A weight with a gradient sink (``w._kgwe_grad_sink``, set by
+    kgwe.parallel.zero at world > 1) gets its dW written by the GEMM straight
+    into the reduce-scatter bucket; autograd then sees no gradient for it."""
 
     @staticmethod
     def forward(ctx, x, w):
@@ -263,6 +284,7 @@ class _Linear(torch.autograd.Function):
         # Persistent W^T copy kept by the data-parallel wrapper, if any
         # (kgwe.parallel.zero): makes dX = dY W an "nt" GEMM.
         ctx.wt = getattr(w, "_kgwe_wt", None)
+        ctx.sink = getattr(w, "_kgwe_grad_sink", None)
         return torch.nn.functional.linear(x, w)
 
     @staticmethod
@@ -278,15 +300,8 @@ class _Linear(torch.autograd.Function):
             wt = ctx.wt
             dx = (torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)).view(x.shape)
         if ctx.needs_input_grad[1]:
-            mode = _wgrad_mode()
-            if mode != "library" and (N < K or mode == "kernel") and wgrad_supported(dy2, x2):
-                dw = wgrad(dy2, x2)
-            elif x2.shape[0] % 8 or N % 8 or K % 8 or not x2.is_contiguous():
-                dw = torch.mm(dy2.t(), x2)
-            elif N >= K:
-                dw = torch.mm(dy2.t(), transpose(x2).t())   # "tt"
-            else:
-                dw = torch.mm(transpose(dy2), x2)           # "nn"
+            if ctx.sink is None or not ctx.sink(dy2, x2):
+                dw = weight_grad(dy2, x2)
         return dx, dw
 
 

@@ -154,16 +154,18 @@ class Checkpointer:
         saved_world = int(files[0].name.split("-of-")[1].split(".")[0])
         if saved_world == world:
             payload = torch.load(sdir / f"rank{rank}-of-{world}.pt", weights_only=True)
-            if payload["numel"] != [b.numel for b in dp.buckets]:
-                raise ValueError("checkpoint bucket layout does not match this model")
+            _check_layout(payload, dp, world, rank)
             state = {"step": payload["dp_step"], "world": world, "rank": rank,
                      "buckets": payload["buckets"]}
         else:  # elastic: re-slice every saved shard for this rank
             parts = [torch.load(sdir / f"rank{r}-of-{saved_world}.pt", weights_only=True)
                      for r in range(saved_world)]
             payload = parts[0]
-            if payload["numel"] != [b.numel for b in dp.buckets]:
-                raise ValueError("checkpoint bucket layout does not match this model")
+            for r, part in enumerate(parts):  # every saved shard belongs to this model and to one step
+                _check_layout(part, dp, saved_world, r)
+                if part["dp_step"] != payload["dp_step"] or int(part["step"]) != int(payload["step"]):
+                    raise ValueError(f"checkpoint shards of different steps in {sdir} "
+                                     f"(rank 0: {payload['step']}, rank {r}: {part['step']})")
             buckets = []
             for i, b in enumerate(dp.buckets):
                 lo = rank * b.shard
@@ -184,6 +186,29 @@ class Checkpointer:
         state["buckets"] = [{k: t.to(dev) for k, t in b.items()} for b in state["buckets"]]
         dp.load_shard_state(state)
         return {"step": int(payload["step"]), "extra": payload.get("extra") or {}}
+
+
+def _check_layout(payload: dict, dp, world: int, rank: int) -> None:
+    """A saved shard must come from this model's bucket layout: same bucket
+    sizes, the rank / world its file name says, and shards of the length that
+    world implies (a stale or foreign file would otherwise be sliced into the
+    optimizer state silently)."""
+    numel = [b.numel for b in dp.buckets]
+    if list(payload.get("numel", [])) != numel:
+        raise ValueError("checkpoint bucket layout does not match this model "
+                         f"(saved {list(payload.get('numel', []))[:4]}..., model {numel[:4]}...)")
+    if int(payload.get("world", world)) != world or int(payload.get("rank", rank)) != rank:
+        raise ValueError(f"checkpoint shard says rank {payload.get('rank')} of {payload.get('world')}, "
+                         f"its file name rank {rank} of {world}")
+    if len(payload["buckets"]) != len(numel):
+        raise ValueError("checkpoint has a different number of buckets than this model")
+    for i, (n, saved) in enumerate(zip(numel, payload["buckets"])):
+        align = world * 64
+        shard = -(-n // align) * align // world
+        for k in ("master", "m", "v"):
+            if k not in saved or saved[k].numel() != shard:
+                raise ValueError(f"checkpoint bucket {i} '{k}' has {saved[k].numel() if k in saved else 0} "
+                                 f"elements, a {world}-rank shard of {n} has {shard}")
 
 
 class _null:

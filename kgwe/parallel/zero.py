@@ -9,10 +9,16 @@ gradient (ZeRO-2):
 * parameters live in a few large flat bf16 **buckets** (~100 M elements,
   backward order); every ``nn.Parameter`` is a view into one, so the model
   code is unchanged;
-* backward: a post-accumulate-grad hook copies each gradient into its
-  bucket's fp32 (or bf16) gradient buffer and frees it; when a bucket is
-  complete its **reduce-scatter** is issued asynchronously over RCCL, so the
-  collectives of early buckets overlap the rest of backward;
+* backward: with the default bf16 reduce, each linear layer's
+  weight-gradient GEMM writes straight into its slice of the bucket's
+  gradient buffer (``_grad_sink``: no gradient tensor, no copy); the few
+  other parameters (norms, embedding) and the fp32-reduce option go through
+  a post-accumulate-grad hook that copies the gradient in and frees it.  When
+  a bucket is complete its **reduce-scatter** is issued asynchronously over
+  RCCL, so the collectives of early buckets overlap the rest of backward.
+  bf16 reduction halves the bytes on the xGMI ring; it perturbs the update no
+  more than the bf16 rounding of the local gradients already does (bounded
+  against fp32 reduction for worlds 4 and 8 in tests/test_parallel_cpu.py);
 * update, per bucket, as soon as the bucket's gradients are reduced — still
   inside backward, on a side HIP stream: a multi-tensor HIP AdamW launch over
   this rank's shard (fp32 master, m, v; grads averaged through
@@ -40,6 +46,7 @@ training-side implementation the platform places.
 from __future__ import annotations
 
 import contextlib
+import functools
 import os
 
 import torch
@@ -47,6 +54,13 @@ import torch.distributed as dist
 
 from ..ops import functional as K
 from ..ops.adamw import AdamPlan
+
+
+class _Done:
+    """Handle of a collective that has already completed."""
+
+    def wait(self) -> None:
+        pass
 
 
 class _Bucket:
@@ -80,7 +94,7 @@ class ShardedDataParallel:
 
     def __init__(self, model: torch.nn.Module, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, bucket_elems: int = 100 * 2**20,
-                 reduce_dtype: torch.dtype = torch.float32, group=None, overlap_step: bool = True,
+                 reduce_dtype: torch.dtype = torch.bfloat16, group=None, overlap_step: bool = True,
                  transposed_weights: bool = True, background_grid: int | None = None):
         self.model = model
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
@@ -130,6 +144,11 @@ class ShardedDataParallel:
         self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
         self._slot = {id(p): (b, o) for b in self.buckets for p, o in zip(b.params, b.offsets)}
         self._hooks = []
+        # Ranks whose tensors live on a GPU but whose backend is gloo (the
+        # one-GPU rehearsal of the multi-rank path): collectives go through
+        # host memory.
+        self._host_staged = (self.world > 1 and self.device.type == "cuda"
+                             and dist.get_backend(group) == "gloo")
         if self.world > 1 or self.overlap:
             for b in self.buckets:
                 for p in b.params:
@@ -141,6 +160,17 @@ class ShardedDataParallel:
                     uniq = list({id(b): b for b in own}.values())
                     self._hooks.append(mod.register_forward_pre_hook(
                         lambda _m, _a, bs=uniq: self._wait_params(bs)))
+
+        # bf16 reduce: a linear weight's dW GEMM writes straight into the
+        # bucket (kgwe.ops.functional._Linear), so its gradient is never copied.
+        self._sinks = []
+        if self.world > 1 and self.device.type == "cuda" and reduce_dtype == torch.bfloat16:
+            embed = {id(m.weight) for m in model.modules() if isinstance(m, torch.nn.Embedding)}
+            for b in self.buckets:
+                for p in b.params:
+                    if p.dim() == 2 and p.dtype == torch.bfloat16 and id(p) not in embed:
+                        p._kgwe_grad_sink = functools.partial(self._grad_sink, p)
+                        self._sinks.append(p)
 
     # ------------------------------------------------------------ layout
     def _make_bucket(self, params) -> _Bucket:
@@ -206,11 +236,24 @@ class ShardedDataParallel:
 
     # ------------------------------------------------------------ backward
     @torch.no_grad()
+    def _grad_sink(self, p: torch.nn.Parameter, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+        """Called by the linear layer's backward instead of returning dW: the
+        weight-gradient GEMM writes this parameter's slice of the
+        reduce-scatter bucket itself (no gradient tensor, no copy)."""
+        b, o = self._slot[id(p)]
+        K.weight_grad(dy2, x2, out=b.gfull[o:o + p.numel()].view(p.shape))
+        self._param_done(p, b)
+        return True
+
+    @torch.no_grad()
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
         b, o = self._slot[id(p)]
         if self.world > 1:
             b.gfull[o:o + p.numel()].view(p.shape).copy_(p.grad)
             p.grad = None
+        self._param_done(p, b)
+
+    def _param_done(self, p: torch.nn.Parameter, b: _Bucket) -> None:
         if id(p) not in b.seen:
             b.seen.add(id(p))
             b.pending -= 1
@@ -228,8 +271,27 @@ class ShardedDataParallel:
             self._update(b, background=b is not self.buckets[-1])
 
     def _reduce_scatter(self, b: _Bucket) -> None:
+        if self._host_staged:
+            # gloo is given host tensors only: device -> host with a synchronous
+            # copy (which also orders it after the gradients), reduce, and back
+            h = b.gfull.cpu()
+            out = torch.empty(b.shard, dtype=h.dtype)
+            dist.reduce_scatter_tensor(out, h, op=dist.ReduceOp.SUM, group=self.group)
+            b.gshard.copy_(out)
+            b.rs_work = _Done()
+            return
         b.rs_work = dist.reduce_scatter_tensor(b.gshard, b.gfull, op=dist.ReduceOp.SUM,
                                                group=self.group, async_op=True)
+
+    def _all_gather(self, b: _Bucket, s0: int):
+        if self._host_staged:
+            torch.cuda.current_stream(self.device).synchronize()  # the shard's update has finished
+            mine = b.flat[s0:s0 + b.shard].cpu()
+            full = torch.empty(b.padded, dtype=mine.dtype)
+            dist.all_gather_into_tensor(full, mine, group=self.group)
+            b.flat.copy_(full)
+            return _Done()
+        return dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard], group=self.group, async_op=True)
 
     @torch.no_grad()
     def _update(self, b: _Bucket, background: bool = False) -> None:
@@ -254,8 +316,7 @@ class ShardedDataParallel:
                 self._plan.launch([(b.master, b.gshard, b.m, b.v, b.flat[s0:s0 + b.shard])],
                                   self.lr, b1, b2, self.eps, self.wd, self._step,
                                   grad_scale=1.0 / self.world, max_grid=grid)
-                b.ag_work = dist.all_gather_into_tensor(b.flat, b.flat[s0:s0 + b.shard],
-                                                        group=self.group, async_op=True)
+                b.ag_work = self._all_gather(b, s0)
                 if b.tparams and side is not None:
                     b.ag_work.wait()  # the side stream waits for the gathered weights
                     b.ag_work = None
@@ -349,6 +410,8 @@ class ShardedDataParallel:
                 p.grad = None
                 if hasattr(p, "_kgwe_wt"):
                     del p._kgwe_wt
+                if hasattr(p, "_kgwe_grad_sink"):
+                    del p._kgwe_grad_sink
             b.flat = b.master = b.m = b.v = b.gfull = b.gshard = b.flat_t = None
         self.buckets = []
         self._bucket_of.clear()

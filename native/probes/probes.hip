@@ -235,19 +235,93 @@ KGWE_API int kgwe_probe_p2p(int src, int dst, int64_t bytes, int iters, double* 
 // Every device pulls from every peer at once (all links busy).  matrix is
 // ndev*ndev row-major: matrix[dst*ndev+src] = GB/s of that link under full
 // load (diagonal = 0).  Returns the number of links measured.
+namespace {
+
+// Start gate of the all-links probe: one wave per link spins on a flag in
+// pinned host memory until the host raises it, so every link's copies begin
+// together however long the launches took to enqueue.  The wait is bounded
+// (100 MHz wall clock): a flag that never comes costs `limit_ticks`, never a
+// hung queue.  out[0] = 1 if the flag was seen, 0 if the wait timed out.
+__global__ void start_gate_kernel(const int* flag, unsigned long long limit_ticks, int* out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  int seen = 0;
+  while (!(seen = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM))) {
+    if (wall_clock64() - t0 > limit_ticks) break;
+    __builtin_amdgcn_s_sleep(64);
+  }
+  if (out) *out = seen ? 1 : 0;
+}
+
+// Everything the all-links probe allocates, released on every return path.
+struct AllLinks {
+  static constexpr int kMax = 16;
+  int ndev = 0;
+  u32x4* src[kMax] = {};
+  u32x4* dst[kMax][kMax] = {};
+  hipStream_t stream[kMax][kMax] = {};
+  hipEvent_t ev0[kMax][kMax] = {}, ev1[kMax][kMax] = {};
+  int* flag = nullptr;  // pinned host memory, mapped into every device
+  ~AllLinks() {
+    for (int d = 0; d < ndev; ++d) {
+      if (hipSetDevice(d) != hipSuccess) continue;
+      (void)hipDeviceSynchronize();  // nothing of ours is still running when its buffers go
+      for (int s = 0; s < ndev; ++s) {
+        if (stream[d][s]) (void)hipStreamDestroy(stream[d][s]);
+        if (ev0[d][s]) (void)hipEventDestroy(ev0[d][s]);
+        if (ev1[d][s]) (void)hipEventDestroy(ev1[d][s]);
+        if (dst[d][s]) (void)hipFree(dst[d][s]);
+      }
+      if (src[d]) (void)hipFree(src[d]);
+    }
+    if (flag) (void)hipHostFree(flag);
+  }
+};
+
+}  // namespace
+
+// Bounded-wait self test of the start gate on one device: with raise = 0 the
+// flag is never set and the kernel must come back after ~limit_us on its own
+// (returns 0); with raise = 1 the host raises it and the kernel must see it
+// (returns 1).  Negative: a HIP error.
+KGWE_API int kgwe_probe_gate_selftest(int dev, int raise, int limit_us) {
+  HIPOK(hipSetDevice(dev));
+  int* flag = nullptr;
+  int* out = nullptr;
+  if (hipHostMalloc(&flag, sizeof(int), hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return -1001;
+  if (hipHostMalloc(&out, sizeof(int), hipHostMallocMapped) != hipSuccess) {
+    (void)hipHostFree(flag);
+    return -1001;
+  }
+  *flag = 0;
+  *out = -1;
+  hipLaunchKernelGGL(start_gate_kernel, dim3(1), dim3(64), 0, 0, flag,
+                     static_cast<unsigned long long>(limit_us) * 100ull, out);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && raise) __atomic_store_n(flag, 1, __ATOMIC_RELEASE);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  const int seen = *out;
+  (void)hipHostFree(flag);
+  (void)hipHostFree(out);
+  return e == hipSuccess ? seen : -static_cast<int>(e) - 1000;
+}
+
+// All ordered pairs at once: matrix[dst * ndev + src] = GB/s of dst pulling
+// from src while every other link of the node is busy too (what a ring or
+// all-to-all collective sees).  Returns the number of links measured.
 KGWE_API int kgwe_probe_p2p_all(int ndev, int64_t bytes, int iters, double* matrix) {
   const int64_t n = bytes / 16;
-  const int maxd = 16;
-  if (ndev > maxd) ndev = maxd;
-  u32x4* srcbuf[maxd] = {};
-  u32x4* dstbuf[maxd][maxd] = {};
-  hipStream_t streams[maxd][maxd] = {};
-  hipEvent_t ev0[maxd][maxd], ev1[maxd][maxd];
+  if (ndev > AllLinks::kMax) ndev = AllLinks::kMax;
+  if (ndev < 1 || n < 1 || iters < 1) return 0;
+  AllLinks r;
+  r.ndev = ndev;
   int links = 0;
+  HIPOK(hipHostMalloc(&r.flag, sizeof(int), hipHostMallocMapped | hipHostMallocPortable));
+  *r.flag = 0;
   for (int d = 0; d < ndev; ++d) {
     HIPOK(hipSetDevice(d));
-    HIPOK(hipMalloc(&srcbuf[d], n * 16));
-    HIPOK(hipMemset(srcbuf[d], d + 1, n * 16));
+    HIPOK(hipMalloc(&r.src[d], n * 16));
+    HIPOK(hipMemset(r.src[d], d + 1, n * 16));
   }
   for (int d = 0; d < ndev; ++d) {
     HIPOK(hipSetDevice(d));
@@ -259,47 +333,52 @@ KGWE_API int kgwe_probe_p2p_all(int ndev, int64_t bytes, int iters, double* matr
       if (!can) continue;
       hipError_t pe = hipDeviceEnablePeerAccess(s, 0);
       if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) continue;
-      HIPOK(hipMalloc(&dstbuf[d][s], n * 16));
-      HIPOK(hipStreamCreateWithFlags(&streams[d][s], hipStreamNonBlocking));
-      HIPOK(hipEventCreate(&ev0[d][s]));
-      HIPOK(hipEventCreate(&ev1[d][s]));
+      (void)hipGetLastError();
+      HIPOK(hipMalloc(&r.dst[d][s], n * 16));
+      HIPOK(hipStreamCreateWithFlags(&r.stream[d][s], hipStreamNonBlocking));
+      HIPOK(hipEventCreate(&r.ev0[d][s]));
+      HIPOK(hipEventCreate(&r.ev1[d][s]));
     }
   }
   for (int d = 0; d < ndev; ++d) {
     HIPOK(hipSetDevice(d));
     HIPOK(hipDeviceSynchronize());
   }
-  // Each link gets 1/7 of the CUs' worth of workgroups so all run together.
-  for (int d = 0; d < ndev; ++d) {
-    HIPOK(hipSetDevice(d));
+  // Every link: gate, timed copies.  Each link gets 1/(ndev-1) of the CUs'
+  // worth of workgroups so all of a device's pulls are resident together.  The
+  // gate waits at most 2 s for the host's flag (raised right after the last
+  // launch below).
+  const unsigned long long gate_ticks = 200000000ull;
+  hipError_t launch_err = hipSuccess;
+  for (int d = 0; d < ndev && launch_err == hipSuccess; ++d) {
+    if ((launch_err = hipSetDevice(d)) != hipSuccess) break;
     const int grid = grid_for(d) / (ndev > 1 ? ndev - 1 : 1);
     for (int s = 0; s < ndev; ++s) {
-      if (!streams[d][s]) continue;
-      HIPOK(hipEventRecord(ev0[d][s], streams[d][s]));
+      if (!r.stream[d][s]) continue;
+      hipLaunchKernelGGL(start_gate_kernel, dim3(1), dim3(64), 0, r.stream[d][s], r.flag, gate_ticks,
+                         static_cast<int*>(nullptr));
+      if ((launch_err = hipEventRecord(r.ev0[d][s], r.stream[d][s])) != hipSuccess) break;
       for (int it = 0; it < iters; ++it)
-        hipLaunchKernelGGL(lds_pull_kernel, dim3(grid > 0 ? grid : 1), dim3(kThreads), 0,
-                           streams[d][s], srcbuf[s], dstbuf[d][s], n);
-      HIPOK(hipEventRecord(ev1[d][s], streams[d][s]));
+        hipLaunchKernelGGL(lds_pull_kernel, dim3(grid > 0 ? grid : 1), dim3(kThreads), 0, r.stream[d][s],
+                           r.src[s], r.dst[d][s], n);
+      if ((launch_err = hipEventRecord(r.ev1[d][s], r.stream[d][s])) != hipSuccess) break;
+      if ((launch_err = hipGetLastError()) != hipSuccess) break;
     }
   }
+  // Raise the flag whatever happened above: gates already enqueued must not
+  // sit out their 2 s before the cleanup's synchronize.
+  __atomic_store_n(r.flag, 1, __ATOMIC_RELEASE);
+  if (launch_err != hipSuccess) return -static_cast<int>(launch_err) - 1000;
   for (int d = 0; d < ndev; ++d) {
     HIPOK(hipSetDevice(d));
     for (int s = 0; s < ndev; ++s) {
-      if (!streams[d][s]) continue;
-      HIPOK(hipEventSynchronize(ev1[d][s]));
+      if (!r.stream[d][s]) continue;
+      HIPOK(hipEventSynchronize(r.ev1[d][s]));
       float ms = 0.f;
-      HIPOK(hipEventElapsedTime(&ms, ev0[d][s], ev1[d][s]));
+      HIPOK(hipEventElapsedTime(&ms, r.ev0[d][s], r.ev1[d][s]));
       matrix[d * ndev + s] = static_cast<double>(n * 16) * iters / (ms * 1e-3) / 1e9;
       ++links;
-      (void)hipStreamDestroy(streams[d][s]);
-      (void)hipEventDestroy(ev0[d][s]);
-      (void)hipEventDestroy(ev1[d][s]);
-      (void)hipFree(dstbuf[d][s]);
     }
-  }
-  for (int d = 0; d < ndev; ++d) {
-    HIPOK(hipSetDevice(d));
-    (void)hipFree(srcbuf[d]);
   }
   return links;
 }

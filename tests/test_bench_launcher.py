@@ -56,9 +56,9 @@ def test_bench_gpus4_rehearses_the_multi_rank_path():
     assert out["config"]["global_batch"] == 4
     assert len(out["loss_per_rank"]) == 4 and len(set(out["loss_per_rank"])) == 4
     assert out["fsdp_row"]["parallelism"] == "fsdp4" and "error" not in out["fsdp_row"]
-    assert out["config"]["grad_reduce_dtype"] == "fp32"
-    rr = out["reduce_dtype_row"]  # the bf16-reduce row ran (or says why not)
-    assert rr.get("grad_reduce_dtype") == "bf16" or "error" in rr, rr
+    assert out["config"]["grad_reduce_dtype"] == "bf16"
+    rr = out["reduce_dtype_row"]  # the fp32-reduce row ran (or says why not)
+    assert rr.get("grad_reduce_dtype") == "fp32" or "error" in rr, rr
 
 
 def test_bench_gpus8_rehearses_the_drivers_headline_point():
@@ -77,7 +77,7 @@ def test_bench_gpus8_rehearses_the_drivers_headline_point():
     assert len(out["util_per_rank"]) == 8
     assert out["fsdp_row"]["parallelism"] == "fsdp8" and "error" not in out["fsdp_row"]
     rr = out["reduce_dtype_row"]
-    assert rr.get("grad_reduce_dtype") == "bf16" or "error" in rr, rr
+    assert rr.get("grad_reduce_dtype") == "fp32" or "error" in rr, rr
     # whole-job rate: 8 ranks x 64 tokens per step
     assert abs(out["tokens_per_s"] - 8 * 64 / (out["ms_per_step"] / 1e3)) < 0.02 * out["tokens_per_s"]
     assert abs(out["tokens_per_s_per_gpu"] * 8 - out["tokens_per_s"]) < 0.02 * out["tokens_per_s"]

@@ -78,6 +78,50 @@ def test_elastic_resume_two_ranks_to_one(tmp_path):
         dist.destroy_process_group()
 
 
+def test_load_refuses_shards_of_another_layout_or_step(tmp_path):
+    """A shard file that does not belong — truncated tensors, a different
+    bucket layout, a rank file copied over another, shards of two different
+    steps — is refused, for the same rank count and for the elastic path."""
+    _run(2, str(tmp_path / "d"), 2, 0, str(tmp_path / "two"))
+    os.environ.pop("WORLD_SIZE", None)
+    os.environ.pop("RANK", None)
+    info = kdist.init(backend="gloo", force_group=False)
+    try:
+        tr = Trainer(_cfg(None), info)
+        sdir = Checkpointer(tmp_path / "d").latest()
+        f0, f1 = sdir / "rank0-of-2.pt", sdir / "rank1-of-2.pt"
+        good0 = torch.load(f0, weights_only=True)
+        good1 = torch.load(f1, weights_only=True)
+        assert Checkpointer(tmp_path / "d").load(tr.dp)["step"] == 2   # intact: loads
+
+        def expect(match):
+            with pytest.raises(ValueError, match=match):
+                Checkpointer(tmp_path / "d").load(tr.dp)
+
+        bad = {**good1, "buckets": [{k: v[:-64] for k, v in b.items()} for b in good1["buckets"]]}
+        torch.save(bad, f1)
+        expect("elements")
+        torch.save({**good1, "numel": [n + 64 for n in good1["numel"]]}, f1)
+        expect("bucket layout")
+        torch.save(good0, f1)                      # rank 0's file copied over rank 1's
+        expect("file name")
+        torch.save({**good1, "step": 7, "dp_step": 7}, f1)
+        expect("different steps")
+        torch.save(good1, f1)
+        # same rank count: a one-rank checkpoint whose tensors were cut short
+        one = tmp_path / "e"
+        ck = Checkpointer(one)
+        ck.save(tr.dp, 5, blocking=True)
+        f = ck.latest() / "rank0-of-1.pt"
+        p = torch.load(f, weights_only=True)
+        torch.save({**p, "buckets": [{k: v[:-64] for k, v in b.items()} for b in p["buckets"]]}, f)
+        with pytest.raises(ValueError, match="elements"):
+            Checkpointer(one).load(tr.dp)
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
 @pytest.mark.gpu
 def test_gpu_checkpoint_side_stream_roundtrip(tmp_path):
     """cuda:0, one process: the pinned side-stream D2H snapshot + background

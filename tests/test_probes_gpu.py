@@ -25,3 +25,21 @@ def test_p2p_probe_pair():
 
     bw = probes.probe_p2p(1, 0, 256 << 20, 5)
     assert bw is not None and bw > 10.0
+
+
+def test_all_links_start_gate_sees_the_flag_and_its_wait_is_bounded():
+    """Every link of the all-links xGMI probe starts behind a gate kernel that
+    waits for one host flag.  Raised: the gate sees it.  Never raised: the gate
+    gives up after its limit by itself (2 ms here), so a lost flag can never
+    park a queue."""
+    import time
+
+    from kgwe.agent import probes
+
+    assert probes.gate_selftest(0, raise_flag=True, limit_us=2_000_000) == 1
+    t0 = time.perf_counter()
+    assert probes.gate_selftest(0, raise_flag=False, limit_us=2000) == 0
+    assert time.perf_counter() - t0 < 1.0
+    # one device has no peer: the all-links probe measures nothing and releases everything
+    if probes.device_count() == 1:
+        assert probes.probe_p2p_all(1, 1 << 20, 1) == [[0.0]]

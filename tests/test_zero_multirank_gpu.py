@@ -2,10 +2,11 @@
 
 RCCL refuses two ranks on one GPU, so this runs the gloo backend with both
 ranks' tensors on cuda:0: the same hooks, side-stream AdamW, per-bucket
-reduce-scatter / all-gather (gloo's CUDA work is ordered against the
-issuing stream like RCCL's), transposed weight copies and forward waits as
-the 8-GPU RCCL run — checked against one process that sees both ranks'
-batches.  Two ranks only (box limit: 16 GPU processes).
+reduce-scatter / all-gather, gradient sinks, transposed weight copies and
+forward waits as the 8-GPU RCCL run — checked against one process that sees
+both ranks' batches.  gloo only ever sees host tensors: the wrapper stages its
+collectives through host memory when the backend is gloo and the tensors are
+on a GPU.  Two ranks only (box limit: 16 GPU processes).
 """
 from __future__ import annotations
 
@@ -34,22 +35,25 @@ def _batches():
     return [torch.randint(0, 1024, (2, 257), generator=g) for _ in range(STEPS)]
 
 
-def _model():
+def _model(dtype=torch.float32):
     from kgwe.models import llama
 
     torch.manual_seed(0)
-    return llama.build("tiny", device="cuda:0", dtype=torch.float32)
+    return llama.build("tiny", device="cuda:0", dtype=dtype)
 
 
-def _rank_main(rank, world, port, out):
+def _rank_main(rank, world, port, out, dtype=torch.float32):
     from kgwe.parallel.zero import ShardedDataParallel
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        m = _model()
+        m = _model(dtype)
         dp = ShardedDataParallel(m, lr=LR, bucket_elems=1 << 19)
+        assert dp._host_staged
+        if dtype == torch.bfloat16:  # the HIP linear path: dW GEMMs write into the buckets
+            assert len(dp._sinks) >= 4 * m.cfg.n_layers
         for tok in _batches():
             mine = tok[rank:rank + 1].cuda()
             loss = m(mine[:, :-1], mine[:, 1:])
@@ -62,7 +66,8 @@ def _rank_main(rank, world, port, out):
                 assert torch.equal(p._kgwe_wt, p.detach().t())
         torch.save({"flat": [b.flat.cpu() for b in dp.buckets],
                     "master": [b.master.cpu() for b in dp.buckets],
-                    "numel": [b.numel for b in dp.buckets]}, f"{out}/rank{rank}.pt")
+                    "numel": [b.numel for b in dp.buckets],
+                    "sinks": len(dp._sinks)}, f"{out}/rank{rank}.pt")
     finally:
         dist.destroy_process_group()
 
@@ -91,3 +96,35 @@ def test_sharded_dp_two_ranks_on_one_gpu_matches_single_process(tmp_path):
         d = (got - want).abs()
         assert d.mean().item() < 0.02 * LR * STEPS, (i, d.mean().item())
         assert (d > 0.5 * LR).float().mean().item() < 0.01, i
+
+
+def test_bf16_ranks_write_weight_gradients_straight_into_the_buckets(tmp_path):
+    """bf16 model, bf16 reduce (the bench's configuration): every linear
+    weight has a gradient sink, its dW GEMM writes the reduce-scatter bucket
+    in place, and the result matches one process that sees both batches."""
+    if not dist.is_gloo_available():
+        pytest.skip("gloo backend not built")
+    mp.spawn(_rank_main, args=(2, _port(), str(tmp_path), torch.bfloat16), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert r0["sinks"] > 0
+    for a, b in zip(r0["flat"], r1["flat"]):
+        assert torch.equal(a, b)
+    from kgwe.parallel.zero import ShardedDataParallel
+
+    m = _model(torch.bfloat16)
+    dp = ShardedDataParallel(m, lr=LR, bucket_elems=1 << 19, overlap_step=False)
+    assert not dp._sinks  # one rank: autograd's gradients are read in place
+    for tok in _batches():
+        t = tok.cuda()
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        dp.step()
+    dp.wait_params()
+    for i, b in enumerate(dp.buckets):
+        got = torch.cat([r0["master"][i], r1["master"][i]])[:b.numel]
+        want = b.master[:b.numel].cpu()
+        d = (got - want).abs()
+        # bf16 activations and gradients: rounding differs between a batch of 2 and two of 1
+        assert d.mean().item() < 0.1 * LR * STEPS, (i, d.mean().item())
+        assert (d > 0.5 * LR).float().mean().item() < 0.05, i
