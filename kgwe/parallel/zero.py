@@ -249,6 +249,11 @@ class ShardedDataParallel:
     def _grad_ready(self, p: torch.nn.Parameter) -> None:
         b, o = self._slot[id(p)]
         if self.world > 1:
+            if p.grad is None:
+                # autograd ran the accumulate node without a gradient: the
+                # linear layer's backward gave it to the sink instead, which
+                # has already marked the parameter done
+                return
             b.gfull[o:o + p.numel()].view(p.shape).copy_(p.grad)
             p.grad = None
         self._param_done(p, b)
