@@ -446,8 +446,86 @@ def run(nodes: int = 16, days: float = 5.0, warmup_days: float = 1.0, seed: int 
     }
 
 
+_T95 = {2: 12.706, 3: 4.303, 4: 3.182, 5: 2.776, 6: 2.571, 7: 2.447, 8: 2.365, 9: 2.306, 10: 2.262}
+
+
+def _mean_ci(xs: list) -> dict | None:
+    """Mean and the half-width of its 95 % confidence interval (Student t)."""
+    xs = [x for x in xs if x is not None]
+    if not xs:
+        return None
+    n = len(xs)
+    m = sum(xs) / n
+    if n < 2:
+        return {"mean": round(m, 3), "ci95": None, "n": n}
+    sd = math.sqrt(sum((x - m) ** 2 for x in xs) / (n - 1))
+    return {"mean": round(m, 3), "ci95": round(_T95.get(n, 1.96) * sd / math.sqrt(n), 3), "n": n,
+            "min": round(min(xs), 3), "max": round(max(xs), 3)}
+
+
+def _one(args) -> dict:
+    nodes, days, warmup, seed, load = args
+    return run(nodes, days, warmup, seed, load)
+
+
+SWEEP_KEYS = ("cluster_busy_util_pct", "cluster_alloc_util_pct", "cost_per_training_run_usd",
+              "usd_per_inference_pod_hour", "usd_per_work_gpu_hour", "fsdp8_wait_min_p99", "wait_min_p99",
+              "multi_pod_allreduce_busbw_gbps_mean", "completed_gpu_hours_of_work", "slice_util_pct",
+              "free_8gpu_islands_avg")
+
+
+def sweep(nodes: int, days: float, warmup_days: float, seeds: list, loads: list, workers: int = 4) -> dict:
+    """The A/B over arrival-rate multipliers and trace seeds: per load, the
+    mean and 95 % CI over seeds of each column's metrics and of the
+    kgwe / stock ratios (each ratio taken per seed, on the same trace)."""
+    import multiprocessing as mp
+
+    todo = [(nodes, days, warmup_days, s, ld) for ld in loads for s in seeds]
+    with mp.get_context("fork").Pool(max(1, workers)) as pool:
+        res = pool.map(_one, todo, chunksize=1)
+    out = {"fleet": f"{nodes} x 8 MI355X", "simulated_days": days, "warmup_days": warmup_days,
+           "seeds": seeds, "loads": loads, "by_load": {}, "model": res[0]["model"]}
+    for ld in loads:
+        rs = [r for r, t in zip(res, todo) if t[4] == ld]
+        row = {"jobs_in_trace": _mean_ci([r["jobs_in_trace"] for r in rs]),
+               "stock": {k: _mean_ci([r["stock"].get(k) for r in rs]) for k in SWEEP_KEYS},
+               "kgwe": {k: _mean_ci([r["kgwe"].get(k) for r in rs]) for k in SWEEP_KEYS},
+               "ratios": {k: _mean_ci([r["ratios"].get(k) for r in rs]) for k in rs[0]["ratios"]},
+               "kgwe_wins_busy_util_in_seeds": sum(1 for r in rs if (r["ratios"]["busy_util"] or 0) > 1.0)}
+        out["by_load"][str(ld)] = row
+    return out
+
+
+def sweep_markdown(sw: dict) -> str:
+    def f(c, unit="", nd=1):
+        if not c:
+            return "n/a"
+        ci = f" ± {c['ci95']:.{nd}f}" if c.get("ci95") is not None else ""
+        return f"{c['mean']:.{nd}f}{ci}{unit}"
+
+    lines = [f"Fleet {sw['fleet']}, {sw['simulated_days']} simulated days after {sw['warmup_days']} warm-up, "
+             f"seeds {sw['seeds']} (mean ± 95 % CI over seeds; ratios are kgwe / stock per seed).", "",
+             "| load | jobs | busy util stock | busy util kgwe | **ratio** | cost / training run ratio | "
+             "$ / inference pod-hour ratio | fsdp8 wait p99 stock → kgwe (min) | all-reduce busBW ratio | "
+             "completed work ratio |", "|---|---|---|---|---|---|---|---|---|---|"]
+    for ld, row in sw["by_load"].items():
+        st, kg, ra = row["stock"], row["kgwe"], row["ratios"]
+        lines.append(
+            f"| {ld}x | {f(row['jobs_in_trace'], nd=0)} | {f(st['cluster_busy_util_pct'], ' %')} | "
+            f"{f(kg['cluster_busy_util_pct'], ' %')} | **{f(ra['busy_util'], 'x', 3)}** | "
+            f"{f(ra['cost_per_training_run'], 'x', 3)} | {f(ra['cost_per_inference_pod_hour'], 'x', 3)} | "
+            f"{f(st['fsdp8_wait_min_p99'], nd=0)} → {f(kg['fsdp8_wait_min_p99'], nd=0)} | "
+            f"{f(ra['allreduce_busbw'], 'x', 2)} | {f(ra['completed_work'], 'x', 3)} |")
+    return "\n".join(lines) + "\n"
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="kgwe bench-cluster")
+    ap.add_argument("--sweep", action="store_true", help="loads x seeds, with confidence intervals")
+    ap.add_argument("--loads", default="0.5,0.75,1.0,1.5,2.0")
+    ap.add_argument("--seeds", default="11,12,13,14,15")
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--markdown", default="", help="with --sweep: also write the table to this file")
     ap.add_argument("--nodes", type=int, default=16)
     ap.add_argument("--days", type=float, default=5.0)
     ap.add_argument("--warmup-days", type=float, default=1.0)
@@ -456,6 +534,14 @@ def main(argv=None) -> int:
     ap.add_argument("--no-consolidate", action="store_true")
     ap.add_argument("--json", action="store_true")
     a = ap.parse_args(argv)
+    if a.sweep:
+        out = sweep(a.nodes, a.days, a.warmup_days, [int(x) for x in a.seeds.split(",")],
+                    [float(x) for x in a.loads.split(",")], a.workers)
+        if a.markdown:
+            with open(a.markdown, "w") as fh:
+                fh.write(sweep_markdown(out))
+        print(json.dumps(out) if a.json else json.dumps(out, indent=1), flush=True)
+        return 0
     out = run(a.nodes, a.days, a.warmup_days, a.seed, a.load, consolidate=not a.no_consolidate)
     print(json.dumps(out) if a.json else json.dumps(out, indent=1), flush=True)
     return 0

@@ -52,3 +52,20 @@ def test_no_consolidation_is_worse():
     on = cluster.run(nodes=8, days=1.5, warmup_days=0.5, seed=11, consolidate=True)
     assert off["kgwe"]["migrations"] == 0
     assert on["kgwe"]["slice_util_pct"] > off["kgwe"]["slice_util_pct"]
+
+
+def test_sweep_pairs_runs_per_seed_and_reports_confidence_intervals():
+    from kgwe.bench import cluster
+
+    sw = cluster.sweep(nodes=4, days=0.5, warmup_days=0.1, seeds=[1, 2, 3], loads=[0.5, 1.5], workers=2)
+    assert list(sw["by_load"]) == ["0.5", "1.5"]
+    for row in sw["by_load"].values():
+        r = row["ratios"]["busy_util"]
+        assert r["n"] == 3 and r["ci95"] is not None and r["min"] <= r["mean"] <= r["max"]
+        assert row["stock"]["cluster_busy_util_pct"]["n"] == 3
+    # more arrivals, more jobs
+    assert sw["by_load"]["1.5"]["jobs_in_trace"]["mean"] > sw["by_load"]["0.5"]["jobs_in_trace"]["mean"]
+    md = cluster.sweep_markdown(sw)
+    assert md.count("\n") >= 5 and "| 0.5x |" in md and "±" in md
+    assert cluster._mean_ci([2.0, 4.0]) == {"mean": 3.0, "ci95": round(12.706 * 2 ** 0.5 / 2 ** 0.5, 3), "n": 2,
+                                            "min": 2.0, "max": 4.0}
