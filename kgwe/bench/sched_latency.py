@@ -172,6 +172,10 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
     sched_cfg = ({"preemptionWaitWindowSeconds": 0.2 * mean_lifetime_s,
                   "preemptionMaxWaitSeconds": mean_lifetime_s} if mean_lifetime_s > 0 else {})
     plat = Platform({"enforceBudgets": True, "partitionReclaimIdleSeconds": reclaim_idle_s,
+                     # consolidation's hysteresis and per-pod cooldown, scaled the same way
+                     # (production: 120 s below 75 % occupancy, one move per pod per hour)
+                     "partitionConsolidateAfterSeconds": reclaim_idle_s,
+                     "migrationCooldownSeconds": 4.0 * reclaim_idle_s,
                      "scheduler": sched_cfg})
     for i in range(n_nodes):
         name = f"mi355x-{i:03d}"

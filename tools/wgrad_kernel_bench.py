@@ -44,6 +44,10 @@ def main():
             variants["lib + transpose(x) [in-step today]"] = lambda: torch.mm(dy.t(), F.transpose(x).t())
         else:
             variants["lib + transpose(dy) [in-step today]"] = lambda: torch.mm(F.transpose(dy), x)
+        # both operands transposed: the library's fastest ("nt") layout, at the price of two transposes
+        variants["lib nt + transpose(dy) + transpose(x)"] = lambda: torch.mm(F.transpose(dy), F.transpose(x).t())
+        dyt, xt = F.transpose(dy), F.transpose(x)
+        variants["lib nt alone (operands pre-transposed)"] = lambda: torch.mm(dyt, xt.t())
         for s in [int(v) for v in a.splits.split(",")]:
             variants[f"kgwe wgrad splits={s or 'auto'}"] = (lambda s=s: wgrad(dy, x, splits=s))
         ref = torch.mm(dy.t(), x).float()
