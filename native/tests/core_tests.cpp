@@ -12,6 +12,7 @@
 // (no GPU or slice ever has two owners, everything is released at the end);
 // under TSan any unsynchronised access fails the run.
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +28,8 @@
 #include "discovery.h"
 #include "hal.h"
 #include "histogram.h"
+#include "http_client.h"
+#include "http_server.h"
 #include "metrics.h"
 #include "partition.h"
 #include "platform.h"
@@ -337,6 +340,164 @@ static void test_concurrent_ledger_stress(int threads, int iters) {
   std::printf("  stress: %d threads x %d iters, %d scheduled\n", threads, iters, scheduled.load());
 }
 
+// Preemption from many threads on a full fleet: planning walks the ledger
+// under the shared lock while binds, releases and other preemptions take the
+// exclusive one.  Non-preemptible work must survive everything.
+static void test_concurrent_preemption(int threads, int iters) {
+  PlatformConfig cfg;
+  cfg.sched.preemption_wait_window_s = 0.0;
+  cfg.sched.preemption_max_rate_percent = 0.0;  // no cap: as many preemptions as the load asks for
+  cfg.sched.preemption_candidate_nodes = 3;
+  auto p = make_platform(12, cfg);
+  Scheduler& s = *p->scheduler();
+  std::set<std::string> pinned;
+  for (int n = 0; n < 12; ++n) {
+    WorkloadRequest keep = gpus("keep" + std::to_string(n), 2, false);
+    keep.preemptible = false;
+    keep.priority = 1;
+    keep.node_selector["kubernetes.io/hostname"] = "n" + std::to_string(n);
+    CHECK(s.schedule(keep).ok);
+    pinned.insert(keep.uid);
+    for (int k = 0; k < 3; ++k) {
+      WorkloadRequest low = gpus("low" + std::to_string(n) + "-" + std::to_string(k), 2, false);
+      low.priority = 1 + k;
+      low.node_selector = keep.node_selector;
+      CHECK(s.schedule(low).ok);
+    }
+  }
+  std::atomic<int> violations{0}, preempted{0}, placed{0};
+  std::vector<std::thread> pool;
+  std::vector<std::string> all_nodes;
+  for (int n = 0; n < 12; ++n) all_nodes.push_back("n" + std::to_string(n));
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      std::mt19937 rng(99 + t);
+      std::vector<std::string> mine;
+      for (int i = 0; i < iters; ++i) {
+        const std::string uid = "hi" + std::to_string(t) + "-" + std::to_string(i);
+        WorkloadRequest w = gpus(uid, 1 << (rng() % 3), false);
+        w.priority = 100 + static_cast<int>(rng() % 50);
+        if (rng() % 4 == 0) {  // the extender's dry run
+          for (const auto& kv : s.preemption_plans(w, all_nodes))
+            for (const auto& v : kv.second)
+              if (pinned.count(v)) ++violations;
+          continue;
+        }
+        Decision d = s.schedule(w);
+        for (const auto& v : d.preempted) {
+          ++preempted;
+          if (pinned.count(v)) ++violations;
+        }
+        if (d.ok) {
+          ++placed;
+          mine.push_back(uid);
+        }
+        if (mine.size() > 2) {
+          if (!s.release(mine.front())) {
+            // released behind our back = preempted by a higher priority: fine
+          }
+          mine.erase(mine.begin());
+        }
+        if (!ledger_consistent(s)) ++violations;
+      }
+      for (const auto& u : mine) (void)s.release(u);
+    });
+  for (auto& th : pool) th.join();
+  CHECK(violations.load() == 0);
+  CHECK(preempted.load() > 0 && placed.load() > 0);
+  for (const auto& k : pinned) CHECK(s.allocation(k, nullptr));  // never evicted
+  CHECK(ledger_consistent(s));
+  CHECK(s.metrics().preemptions >= static_cast<uint64_t>(preempted.load()));
+  std::printf("  preemption: %d threads x %d iters, %d placed, %d victims\n", threads, iters, placed.load(),
+              preempted.load());
+}
+
+// The native extender server under concurrent keep-alive clients: filter,
+// prioritize and bind over real sockets, a gang whose members' binds are held
+// until the last one arrives, and a clean stop with connections open.
+static void test_http_server_verbs_and_gang_hold(int clients, int iters) {
+  auto p = make_platform(4);
+  ExtenderHttpServer::Options opt;
+  opt.host = "127.0.0.1";
+  opt.port = 0;
+  opt.workers = 4;
+  opt.gang_hold_ms = 5000;
+  ExtenderHttpServer srv(p, opt);
+  std::atomic<int> sunk{0};
+  srv.set_bind_sink([&](const std::string&, const std::string&) {
+    ++sunk;
+    return std::string();
+  });
+  CHECK(srv.start().empty());
+  const int port = srv.port();
+  CHECK(port > 0);
+  auto pod = [](const std::string& name, int gpus_n, const std::string& gang, int gang_size) {
+    std::string ann = "\"kgwe.amd.com/topology\":\"None\"";
+    if (!gang.empty())
+      ann += ",\"kgwe.amd.com/gang\":\"" + gang + "\",\"kgwe.amd.com/gang-size\":\"" + std::to_string(gang_size) + "\"";
+    return "{\"metadata\":{\"name\":\"" + name + "\",\"namespace\":\"t\",\"uid\":\"u-" + name +
+           "\",\"annotations\":{" + ann + "}},\"spec\":{\"containers\":[{\"resources\":{\"limits\":{\"amd.com/gpu\":\"" +
+           std::to_string(gpus_n) + "\"}}}]}}";
+  };
+  const std::string names = "[\"n0\",\"n1\",\"n2\",\"n3\"]";
+  std::atomic<int> bad{0}, bound{0};
+  auto one_pod = [&](HttpClient& c, const std::string& name, int n, const std::string& gang, int gsize) {
+    std::string body, out;
+    body = "{\"pod\":" + pod(name, n, gang, gsize) + ",\"nodenames\":" + names + "}";
+    if (c.post("/filter", {body}, &out) != 200) return ++bad, false;
+    Json f = Json::parse(out);
+    const auto& passed = f.get("nodenames").items();
+    if (passed.empty()) return false;
+    if (c.post("/prioritize", {body}, &out) != 200 || Json::parse(out).items().size() != 4) return ++bad, false;
+    const std::string node = passed[0].str();
+    body = "{\"podName\":\"" + name + "\",\"podNamespace\":\"t\",\"podUID\":\"u-" + name + "\",\"node\":\"" + node + "\"}";
+    if (c.post("/bind", {body}, &out) != 200) return ++bad, false;
+    if (!Json::parse(out).get("error").str().empty()) return false;
+    ++bound;
+    return true;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 0; t < clients; ++t)
+    pool.emplace_back([&, t] {
+      HttpClient c("127.0.0.1", port, 10.0);
+      for (int i = 0; i < iters; ++i) {
+        const std::string name = "p" + std::to_string(t) + "-" + std::to_string(i);
+        if (one_pod(c, name, 1, "", 0)) (void)p->release("u-" + name, 0.0);
+      }
+    });
+  // meanwhile: a gang of 4 whose members arrive 30 ms apart; every bind must
+  // come back OK, the early ones only after the last member's bind
+  std::vector<std::thread> gang;
+  std::atomic<int> gang_ok{0};
+  std::vector<double> done_ms(4, 0.0);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int m = 0; m < 4; ++m)
+    gang.emplace_back([&, m] {
+      std::this_thread::sleep_for(std::chrono::milliseconds(30 * m));
+      HttpClient c("127.0.0.1", port, 10.0);
+      if (one_pod(c, "g" + std::to_string(m), 2, "ring", 4)) ++gang_ok;
+      done_ms[m] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+  for (auto& th : gang) th.join();
+  for (auto& th : pool) th.join();
+  CHECK(bad.load() == 0);
+  CHECK(gang_ok.load() == 4);
+  CHECK(done_ms[0] >= 85.0);  // held until the member that arrived at 90 ms
+  CHECK(bound.load() >= 4 && sunk.load() == bound.load());
+  CHECK(srv.parked() == 0);
+  const Json st = Json::parse(srv.stats_json());
+  CHECK(st.get("gang_binds_held").as_int(0) >= 3);
+  CHECK(st.get("verbs").get("filter").get("count").as_int(0) >= clients * iters);
+  HttpClient idle("127.0.0.1", port, 5.0);  // an open keep-alive connection at stop
+  std::string out;
+  CHECK(idle.post("/filter", {"{\"pod\":" + pod("z", 1, "", 0) + ",\"nodenames\":" + names + "}"}, &out) == 200);
+  srv.stop();
+  for (int m = 0; m < 4; ++m) (void)p->release("u-g" + std::to_string(m), 0.0);
+  CHECK(ledger_consistent(*p->scheduler()));
+  std::printf("  http: %d clients x %d pods + gang of 4 (held %.0f ms), %d binds\n", clients, iters, done_ms[0],
+              bound.load());
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 400;
   test_topology_fixture();
@@ -349,6 +510,8 @@ int main(int argc, char** argv) {
   test_nodemap_copy_on_write();
   test_metrics_commit_snapshot();
   test_concurrent_ledger_stress(8, iters);
+  test_concurrent_preemption(6, std::max(40, iters / 4));
+  test_http_server_verbs_and_gang_hold(6, std::max(20, iters / 10));
   if (g_failures) {
     std::fprintf(stderr, "%d check(s) failed\n", g_failures);
     return 1;
