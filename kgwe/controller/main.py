@@ -36,6 +36,7 @@ DEFAULTS = {
                   "preemptionMaxRatePercent": 4.0, "preemptionWindowSeconds": 300, "preemptionBurst": 8},
     "webhook": {"port": 8443, "certFile": "", "keyFile": ""},
     "cost": {"journalPath": "", "enableSpotOptimization": True, "enableRightsizing": True},
+    "shareSocketDir": "/run/kgwe/share",
     "partitionDryRun": False,
     "autoProvisionPartitions": True,
     "partitionReclaimIdleSeconds": 60.0,
@@ -59,7 +60,7 @@ DEFAULTS = {
 
 
 def build(cfg: dict):
-    plat = Platform({k: cfg[k] for k in ("scheduler", "cost", "partitionDryRun",
+    plat = Platform({k: cfg[k] for k in ("scheduler", "cost", "partitionDryRun", "shareSocketDir",
                                          "autoProvisionPartitions", "partitionReclaimIdleSeconds",
                                          "enforceBudgets", "partitionConsolidateBelow",
                                          "partitionConsolidateAfterSeconds", "migrationCooldownSeconds")})
