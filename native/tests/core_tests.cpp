@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <random>
 #include <map>
@@ -441,18 +442,29 @@ static void test_http_server_verbs_and_gang_hold(int clients, int iters) {
   };
   const std::string names = "[\"n0\",\"n1\",\"n2\",\"n3\"]";
   std::atomic<int> bad{0}, bound{0};
-  auto one_pod = [&](HttpClient& c, const std::string& name, int n, const std::string& gang, int gsize) {
+  // A scheduling cycle as kube-scheduler runs it; a bind that lost a race for
+  // the node's GPUs ("insufficient free GPUs") is retried like a requeued pod.
+  std::function<bool(HttpClient&, const std::string&, int, const std::string&, int, int)> one_pod;
+  one_pod = [&](HttpClient& c, const std::string& name, int n, const std::string& gang, int gsize, int tries) {
     std::string body, out;
     body = "{\"pod\":" + pod(name, n, gang, gsize) + ",\"nodenames\":" + names + "}";
     if (c.post("/filter", {body}, &out) != 200) return ++bad, false;
     Json f = Json::parse(out);
     const auto& passed = f.get("nodenames").items();
-    if (passed.empty()) return false;
+    if (passed.empty()) {
+      if (!gang.empty()) std::fprintf(stderr, "  gang member %s: no node passed: %s\n", name.c_str(), out.c_str());
+      return false;
+    }
     if (c.post("/prioritize", {body}, &out) != 200 || Json::parse(out).items().size() != 4) return ++bad, false;
-    const std::string node = passed[0].str();
+    const std::string node = passed[std::hash<std::string>{}(name) % passed.size()].str();
     body = "{\"podName\":\"" + name + "\",\"podNamespace\":\"t\",\"podUID\":\"u-" + name + "\",\"node\":\"" + node + "\"}";
     if (c.post("/bind", {body}, &out) != 200) return ++bad, false;
-    if (!Json::parse(out).get("error").str().empty()) return false;
+    const std::string err = Json::parse(out).get("error").str();
+    if (!err.empty()) {
+      if (err.find("insufficient") != std::string::npos && tries > 1) return one_pod(c, name, n, gang, gsize, tries - 1);
+      if (!gang.empty()) std::fprintf(stderr, "  gang member %s: bind answered %s\n", name.c_str(), out.c_str());
+      return false;
+    }
     ++bound;
     return true;
   };
@@ -462,7 +474,7 @@ static void test_http_server_verbs_and_gang_hold(int clients, int iters) {
       HttpClient c("127.0.0.1", port, 10.0);
       for (int i = 0; i < iters; ++i) {
         const std::string name = "p" + std::to_string(t) + "-" + std::to_string(i);
-        if (one_pod(c, name, 1, "", 0)) (void)p->release("u-" + name, 0.0);
+        if (one_pod(c, name, 1, "", 0, 1)) (void)p->release("u-" + name, 0.0);
       }
     });
   // meanwhile: a gang of 4 whose members arrive 30 ms apart; every bind must
@@ -475,7 +487,7 @@ static void test_http_server_verbs_and_gang_hold(int clients, int iters) {
     gang.emplace_back([&, m] {
       std::this_thread::sleep_for(std::chrono::milliseconds(30 * m));
       HttpClient c("127.0.0.1", port, 10.0);
-      if (one_pod(c, "g" + std::to_string(m), 2, "ring", 4)) ++gang_ok;
+      if (one_pod(c, "g" + std::to_string(m), 2, "ring", 4, 5)) ++gang_ok;
       done_ms[m] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     });
   for (auto& th : gang) th.join();
@@ -498,6 +510,111 @@ static void test_http_server_verbs_and_gang_hold(int clients, int iters) {
               bound.load());
 }
 
+// Hostile input on the extender port: truncated and oversized requests, bad
+// chunk framing, binary garbage, pipelined requests, clients that vanish mid
+// request.  The server may answer 400 or close, never crash or wedge; a
+// well-formed request afterwards must still be served.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+static int raw_connect(int port) {
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  timeval tv{2, 0};
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) {
+    close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+static std::string raw_exchange(int port, const std::string& bytes, bool half_close = true) {
+  int fd = raw_connect(port);
+  if (fd < 0) return "<connect failed>";
+  size_t off = 0;
+  while (off < bytes.size()) {
+    ssize_t n = send(fd, bytes.data() + off, bytes.size() - off, MSG_NOSIGNAL);
+    if (n <= 0) break;
+    off += static_cast<size_t>(n);
+  }
+  if (half_close) shutdown(fd, SHUT_WR);
+  std::string out;
+  char buf[4096];
+  for (;;) {
+    ssize_t n = recv(fd, buf, sizeof buf, 0);
+    if (n <= 0) break;
+    out.append(buf, static_cast<size_t>(n));
+    if (out.size() > (1u << 20)) break;
+  }
+  close(fd);
+  return out;
+}
+
+static void test_http_server_hostile_input() {
+  auto p = make_platform(2);
+  ExtenderHttpServer::Options opt;
+  opt.host = "127.0.0.1";
+  opt.port = 0;
+  opt.workers = 3;
+  opt.max_body = 1 << 16;
+  ExtenderHttpServer srv(p, opt);
+  CHECK(srv.start().empty());
+  const int port = srv.port();
+  const std::string good_body = "{\"pod\":{\"metadata\":{\"name\":\"a\",\"uid\":\"ua\"},\"spec\":{\"containers\":[{\"resources\":"
+                                "{\"limits\":{\"amd.com/gpu\":\"1\"}}}]}},\"nodenames\":[\"n0\",\"n1\"]}";
+  auto post = [&](const std::string& path, const std::string& body) {
+    return "POST " + path + " HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(body.size()) +
+           "\r\nConnection: close\r\n\r\n" + body;
+  };
+  auto status = [](const std::string& r) { return r.size() > 12 ? std::atoi(r.c_str() + 9) : 0; };
+  std::vector<std::string> hostile = {
+      "",                                                             // connect and leave
+      "GARBAGE\r\n\r\n",                                            // no request line
+      "POST /filter HTTP/1.1\r\nContent-Length: 100\r\n\r\n{\"pod\":",   // body cut short
+      "POST /filter HTTP/1.1\r\nContent-Length: 99999999999\r\n\r\n",   // over max_body
+      "POST /filter HTTP/1.1\r\nContent-Length: -5\r\n\r\nxx",
+      "POST /filter HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nZZZ\r\nabc\r\n0\r\n\r\n",  // bad chunk size
+      "POST /filter HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nffffffffffffffff\r\n",      // absurd chunk
+      post("/filter", "{not json"),
+      post("/filter", "[]"),
+      post("/bind", "{\"podName\":5}"),
+      post("/preempt", "{\"pod\":null,\"nodeNameToMetaVictims\":7}"),
+      post("/prioritize", std::string(60000, '[')),                      // deep nesting
+      "POST /" + std::string(70000, 'a') + " HTTP/1.1\r\n\r\n",          // header past the limit
+      std::string("POST /filter HTTP/1.1\r\nContent-Length: 4\r\n\r\n\0\xff\xfe\x01", 47),
+  };
+  std::mt19937 rng(7);
+  for (int i = 0; i < 40; ++i) {  // random bytes, some after a plausible request line
+    std::string g(rng() % 600, '\0');
+    for (auto& ch : g) ch = static_cast<char>(rng());
+    hostile.push_back(i % 2 ? "POST /filter HTTP/1.1\r\n" + g : g);
+  }
+  for (const auto& h : hostile) {
+    const std::string r = raw_exchange(port, h);
+    const int st = status(r);
+    CHECK(r.empty() || st == 200 || st == 400 || st == 404 || st == 413 || st == 500);
+  }
+  // 200 replies to hostile JSON carry an error, not a placement
+  CHECK(raw_exchange(port, post("/filter", "{not json")).find("rror") != std::string::npos);
+  // two pipelined requests on one connection, both answered in order
+  const std::string keep = "POST /filter HTTP/1.1\r\nContent-Length: " + std::to_string(good_body.size()) + "\r\n\r\n" + good_body;
+  const std::string two = raw_exchange(port, keep + post("/prioritize", good_body));
+  size_t first = two.find("HTTP/1.1 200"), second = two.find("HTTP/1.1 200", first + 1);
+  CHECK(first != std::string::npos && second != std::string::npos);
+  CHECK(two.find("nodenames") != std::string::npos && two.find("\"host\"") != std::string::npos);
+  // the server is still healthy
+  const std::string ok = raw_exchange(port, post("/filter", good_body));
+  CHECK(status(ok) == 200 && ok.find("\"n0\"") != std::string::npos);
+  srv.stop();
+  std::printf("  http hostile input: %zu cases survived\n", hostile.size());
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 400;
   test_topology_fixture();
@@ -512,6 +629,7 @@ int main(int argc, char** argv) {
   test_concurrent_ledger_stress(8, iters);
   test_concurrent_preemption(6, std::max(40, iters / 4));
   test_http_server_verbs_and_gang_hold(6, std::max(20, iters / 10));
+  test_http_server_hostile_input();
   if (g_failures) {
     std::fprintf(stderr, "%d check(s) failed\n", g_failures);
     return 1;
