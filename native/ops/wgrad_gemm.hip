@@ -24,8 +24,6 @@
 // at its end, one workgroup barrier per K-tile.  Workgroups are numbered so
 // that the 32 tiles resident on one XCD form an 8 x 4 patch sharing A and B
 // panels in that XCD's L2.
-#include <cstdlib>
-
 #include "common.h"
 
 using namespace kgwe;
@@ -228,162 +226,6 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(const bf16_t* __restric
   }
 }
 
-// ---------------------------------------------------------------------------
-// Four-wave form: the same tile, stages and LDS images, but 4 waves (2 x 2)
-// with 128 x 128 of C each = 16 accumulators (256 AGPRs), one wave per SIMD.
-// Per 16-token slice a wave reads 8 operand fragments for 16 MFMAs where the
-// 8-wave form reads 6 for 8: a third less LDS traffic per MFMA, which is what
-// bounds the 8-wave form (transposing reads move 8 bytes per lane).  With no
-// partner wave on the SIMD, the next slice's fragments are always in flight
-// under the current slice's 16 MFMAs.
-// ---------------------------------------------------------------------------
-constexpr int kThreads4 = 256;
-
-template <bool OUT_F32>
-__global__ __launch_bounds__(kThreads4) void wgrad4_kernel(const bf16_t* __restrict__ A,
-                                                           const bf16_t* __restrict__ B, void* __restrict__ Cout,
-                                                           int M, int N, int T, int lda, int ldb, int ldc,
-                                                           int splits) {
-  __shared__ __attribute__((aligned(1024))) char lds0[kStage];
-  __shared__ __attribute__((aligned(1024))) char lds1[kStage];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int tiles_m = M / BM, tiles_n = N / BN;
-  const int ntile = tiles_m * tiles_n;
-  int id = xcd_remap(static_cast<int>(blockIdx.x), ntile * splits);
-  const int split = id % splits;
-  id /= splits;
-  const int per_group = GROUP_M * tiles_n;
-  const int grp = id / per_group;
-  const int first_m = grp * GROUP_M;
-  const int gsz = min(GROUP_M, tiles_m - first_m);
-  const int tm = first_m + (id % per_group) % gsz;
-  const int tn = (id % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nt_all = T / BK;
-  const int per = (nt_all + splits - 1) / splits;
-  const int kt0 = split * per;
-  const int nt = max(0, min(per, nt_all - kt0));
-
-  // ---- LDS-DMA: this wave stages 16 token rows of BOTH 128-column halves ----
-  const int lrow = lane >> 4, cp = lane & 15;
-  const int rg0 = wave * 4;
-  int goffA[2][4], goffB[2][4];
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 4 * (rg0 + i) + lrow;
-      const int ch = cp ^ ((lrow << 2) | i);
-      goffA[hf][i] = row * lda + hf * 128 + ch * 8;
-      goffB[hf][i] = row * ldb + hf * 128 + ch * 8;
-    }
-  const bf16_t* gA = A + static_cast<size_t>(kt0) * BK * lda + m0;
-  const bf16_t* gB = B + static_cast<size_t>(kt0) * BK * ldb + n0;
-  const int lds_ld = rg0 * 1024;
-
-  // ---- transposed-read geometry: as in the 8-wave kernel, all four 32-column blocks of each image ----
-  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, h = G >> 1, rh = G & 1;
-  int off[4][2];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-    for (int part = 0; part < 2; ++part)
-      off[cb][part] = 256 * (8 * h + q + 4 * part) + 16 * ((2 * rh + (p >> 1)) ^ (2 * h + part)) + 8 * (p & 1) +
-                      64 * (cb ^ q);
-  const int imgA = wm * kImage;
-  const int imgB = 2 * kImage + wn * kImage;
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  auto stage = [&](int st, int t, bool b_operand) {
-    const bf16_t* g = (b_operand ? gB : gA) + static_cast<size_t>(t) * BK * (b_operand ? ldb : lda);
-    char* d = (st ? lds1 : lds0) + (b_operand ? 2 * kImage : 0) + lds_ld;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        glds16(g + (b_operand ? goffB[hf][i] : goffA[hf][i]), d + hf * kImage + i * 1024);
-  };
-  auto frags = [&](const char* sa, const char* sb, int R, bf16x8 (&fa)[4], bf16x8 (&fb)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fb[j] = cat44(tr_read(sb + 256 * R + off[j][0]), tr_read(sb + 256 * R + off[j][1]));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      fa[i] = cat44(tr_read(sa + 256 * R + off[i][0]), tr_read(sa + 256 * R + off[i][1]));
-  };
-  auto mma = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
-  };
-  auto ktile = [&](int st, int t) {
-    const char* sa = (st ? lds1 : lds0) + imgA;
-    const char* sb = (st ? lds1 : lds0) + imgB;
-    const bool more = t + 1 < nt;
-    bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
-    frags(sa, sb, 0, fa0, fb0);
-    if (more) stage(st ^ 1, t + 1, false);
-    frags(sa, sb, 16, fa1, fb1);
-    mma(fa0, fb0);
-    if (more) stage(st ^ 1, t + 1, true);
-    frags(sa, sb, 32, fa0, fb0);
-    mma(fa1, fb1);
-    frags(sa, sb, 48, fa1, fb1);
-    mma(fa0, fb0);
-    mma(fa1, fb1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-
-  if (nt > 0) {
-    stage(0, 0, false);
-    stage(0, 0, true);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // nt is even (the launcher falls back to the 8-wave kernel otherwise): no
-    // branch around a K-tile, so the 256 accumulators are never loop phis that
-    // the compiler would shuttle between AGPRs and VGPRs
-    for (int t = 0; t < nt; t += 2) {
-      ktile(0, t);
-      ktile(1, t + 1);
-    }
-  }
-
-  const int crow = m0 + wm * 128 + 4 * (lane >> 5);
-  const int ccol = n0 + wn * 128 + (lane & 31);
-  if (OUT_F32) {
-    float* C = static_cast<float*>(Cout) + static_cast<size_t>(split) * M * ldc;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          C[static_cast<size_t>(crow + 32 * i + (r & 3) + 8 * (r >> 2)) * ldc + ccol + 32 * j] = acc[i][j][r];
-  } else {
-    bf16_t* C = static_cast<bf16_t*>(Cout);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          C[static_cast<size_t>(crow + 32 * i + (r & 3) + 8 * (r >> 2)) * ldc + ccol + 32 * j] =
-              f2bf(acc[i][j][r]);
-  }
-}
-
 // Sum of the split-K slabs -> bf16.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slabs,
                                                            bf16_t* __restrict__ C, int64_t n, int splits) {
@@ -401,17 +243,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   *reinterpret_cast<u4*>(C + i) = o;
 }
 
-}  // namespace
-
-namespace {
-// KGWE_WGRAD_WAVES=4 selects the four-wave form (default: eight waves).
-bool wgrad_four_waves() {
-  static const bool four = [] {
-    const char* e = std::getenv("KGWE_WGRAD_WAVES");
-    return e && e[0] == '4';
-  }();
-  return four;
-}
 }  // namespace
 
 // Split count the launcher will use for C[M, N] over T tokens: whole waves of
@@ -458,23 +289,14 @@ KGWE_API int kgwe_wgrad_bf16(const void* A, const void* B, void* C, void* worksp
   const int tiles = (M / BM) * (N / BN);
   const bf16_t* a = static_cast<const bf16_t*>(A);
   const bf16_t* b = static_cast<const bf16_t*>(B);
-  const int nt_split = (T / BK + splits - 1) / splits;
-  const bool four = wgrad_four_waves() && (T / BK) % splits == 0 && nt_split % 2 == 0;
   if (splits == 1) {
-    if (four)
-      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(tiles), dim3(kThreads4), 0, s, a, b, C, M, N, T, lda, ldb, ldc, 1);
-    else
-      hipLaunchKernelGGL(wgrad_kernel<false>, dim3(tiles), dim3(kThreads), 0, s, a, b, C, M, N, T, lda, ldb, ldc, 1);
+    hipLaunchKernelGGL(wgrad_kernel<false>, dim3(tiles), dim3(kThreads), 0, s, a, b, C, M, N, T, lda, ldb, ldc, 1);
     return KGWE_CHECK_LAUNCH();
   }
   if (!workspace) return -2;
   if (ldc != N) return -1;  // slabs are dense [splits][M][N]
-  if (four)
-    hipLaunchKernelGGL(wgrad4_kernel<true>, dim3(tiles * splits), dim3(kThreads4), 0, s, a, b, workspace, M, N, T,
-                       lda, ldb, N, splits);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<true>, dim3(tiles * splits), dim3(kThreads), 0, s, a, b, workspace, M, N, T, lda,
-                       ldb, N, splits);
+  hipLaunchKernelGGL(wgrad_kernel<true>, dim3(tiles * splits), dim3(kThreads), 0, s, a, b, workspace, M, N, T, lda,
+                     ldb, N, splits);
   if (int rc = KGWE_CHECK_LAUNCH()) return rc;
   const int64_t n = static_cast<int64_t>(M) * N;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>((n / 4 + 255) / 256)), dim3(256), 0, s,
