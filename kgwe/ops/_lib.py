@@ -36,6 +36,8 @@ _SIGS = {
     "kgwe_swiglu_fwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p]),
     "kgwe_swiglu_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                 c_int64, c_int64, c_int, c_void_p]),
+    "kgwe_swiglu_bwd_t": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                  c_int64, c_void_p, c_int64, c_int, c_void_p]),
     "kgwe_rope_qkv_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int64, c_int, c_int, c_int, c_int, c_void_p]),
     "kgwe_rope_qkv_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

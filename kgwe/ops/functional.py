@@ -23,6 +23,36 @@ def _require(cond: bool, msg: str) -> None:
 
 
 # --------------------------------------------------------------------------
+# Transposed gradients handed from a producer's backward to the consuming
+# linear layer's backward
+# --------------------------------------------------------------------------
+# A weight gradient dW = dY^T X reduces over tokens; the library's fastest GEMM
+# layout wants dY^T and X^T (token dimension contiguous).  Transposing dY in
+# a pass of its own costs what the layout gains, so the kernel that PRODUCES
+# dY (SwiGLU backward for the gate|up projection) writes dY^T next to it and
+# offers it here, keyed by dY's storage; the linear layer's backward, the next
+# autograd node to run, takes it.  One entry: an offer nobody took is dropped
+# by the next one.
+_offered: dict = {}
+
+
+def _dual_grads() -> bool:
+    return os.environ.get("KGWE_DUAL_GRADS", "1") != "0"
+
+
+def _offer_transposed(dy: torch.Tensor, dy_t: torch.Tensor) -> None:
+    _offered.clear()
+    # dy itself is held too: while the offer stands its storage cannot be
+    # reused for another tensor that would then match the key
+    _offered[(dy.data_ptr(), dy.shape[0], dy.shape[1], dy.device)] = (dy_t, dy)
+
+
+def _take_transposed(dy2: torch.Tensor) -> torch.Tensor | None:
+    hit = _offered.pop((dy2.data_ptr(), dy2.shape[0], dy2.shape[1], dy2.device), None)
+    return None if hit is None else hit[0]
+
+
+# --------------------------------------------------------------------------
 # RMSNorm (+ fused residual add)
 # --------------------------------------------------------------------------
 class _RMSNorm(torch.autograd.Function):
@@ -106,9 +136,17 @@ class _SwiGLU(torch.autograd.Function):
         d2 = dout.reshape(-1, Fh).contiguous()
         dgu = torch.empty_like(gu2)
         es = gu2.element_size()
-        check(lib().kgwe_swiglu_bwd(ptr(gu2), gu2.data_ptr() + Fh * es, F2, ptr(d2),
-                                    ptr(dgu), dgu.data_ptr() + Fh * es, F2, T, Fh,
-                                    stream(gu2)), "swiglu_bwd")
+        if _dual_grads() and T % 64 == 0 and Fh % 64 == 0:
+            # also the transposed gradient, for the producing projection's dW GEMM
+            dgu_t = torch.empty(F2, T, device=gu2.device, dtype=gu2.dtype)
+            check(lib().kgwe_swiglu_bwd_t(ptr(gu2), gu2.data_ptr() + Fh * es, F2, ptr(d2),
+                                          ptr(dgu), dgu.data_ptr() + Fh * es, F2, ptr(dgu_t), T, Fh,
+                                          stream(gu2)), "swiglu_bwd_t")
+            _offer_transposed(dgu, dgu_t)
+        else:
+            check(lib().kgwe_swiglu_bwd(ptr(gu2), gu2.data_ptr() + Fh * es, F2, ptr(d2),
+                                        ptr(dgu), dgu.data_ptr() + Fh * es, F2, T, Fh,
+                                        stream(gu2)), "swiglu_bwd")
         return dgu.view(ctx.shape)
 
 
@@ -248,6 +286,10 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = 
     the gradient is ever made."""
     N, K = dy2.shape[1], x2.shape[1]
     mode = _wgrad_mode()
+    dy_t = _take_transposed(dy2)
+    if dy_t is not None and mode != "kernel" and x2.is_contiguous() and x2.shape[0] % 8 == 0 and K % 8 == 0:
+        # both operands token-contiguous: the library's "nt" layout
+        return torch.mm(dy_t, transpose(x2).t(), out=out)
     if (mode != "library" and (N < K or mode == "kernel") and wgrad_supported(dy2, x2)
             and (out is None or out.data_ptr() % 8 == 0)):
         return wgrad(dy2, x2, out=out)

@@ -303,3 +303,54 @@ def test_linear_layout_aware_backward_matches_fp32(N, Kd):
     for got, want in ((x.grad, xf.grad), (w.grad, wf.grad)):
         err = (got.float() - want).abs().max().item()
         assert err <= 2e-2 * want.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("T,F,Kd", [(256, 512, 384), (128, 64, 64), (320, 1792, 256)])
+def test_swiglu_backward_hands_its_transposed_gradient_to_the_projection(T, F, Kd, monkeypatch):
+    """FFN up path x -> linear(w13) -> swiglu: the SwiGLU backward writes
+    d(gate|up) and its transpose in one pass and the w13 weight gradient is
+    computed from the transposed copy.  Gradients against an fp32 reference,
+    bit-identical d(gate|up) with the plain backward, transposed copy exact,
+    and nothing left on offer afterwards."""
+    from kgwe.ops import functional as Fn
+
+    torch.manual_seed(11)
+    x = (torch.randn(T, Kd, device=DEV) * 0.5).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(2 * F, Kd, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_()
+    d = torch.randn(T, F, device=DEV).to(torch.bfloat16)
+
+    def run(dual):
+        monkeypatch.setenv("KGWE_DUAL_GRADS", "1" if dual else "0")
+        x.grad = w.grad = None
+        taken = []
+        real = Fn._take_transposed
+
+        def spy(dy2):
+            t = real(dy2)
+            if t is not None:
+                taken.append((t.clone(), dy2.clone()))
+            return t
+        monkeypatch.setattr(Fn, "_take_transposed", spy)
+        K.swiglu(K.linear(x, w)).backward(d)
+        monkeypatch.setattr(Fn, "_take_transposed", real)
+        return x.grad.clone(), w.grad.clone(), taken
+
+    gx1, gw1, taken = run(True)
+    assert len(taken) == 1 and not Fn._offered
+    dy_t, dy = taken[0]
+    assert dy_t.shape == (2 * F, T) and torch.equal(dy_t, dy.t().contiguous())
+    gx0, gw0, none = run(False)
+    assert not none
+    assert torch.equal(gx1, gx0)                      # same d(gate|up), same dX GEMM
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    gu = xf @ wf.t()
+    (torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]).backward(d.float())
+    for got in (gw1, gw0):
+        err = (got.float() - wf.grad).abs().max().item()
+        assert err <= 2e-2 * wf.grad.abs().max().item() + 1e-2, err
+    # a shape the tiled kernel does not take falls back to the plain backward
+    x2 = torch.randn(72, 64, device=DEV).to(torch.bfloat16).requires_grad_()
+    w2 = (torch.randn(2 * 40, 64, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_()
+    monkeypatch.setenv("KGWE_DUAL_GRADS", "1")
+    K.swiglu(K.linear(x2, w2)).sum().backward()
+    assert not Fn._offered and torch.isfinite(w2.grad.float()).all()
