@@ -140,8 +140,9 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(
     for (int j = 0; j < 8; ++j) {
       const float x = bf2f(gv[k][j]), y = bf2f(uv[k][j]), d = bf2f(dv[k][j]);
       const float sgm = sigmoidf_(x);
+      const float silu = x * sgm;  // same operation order as swiglu_bwd_kernel: bit-identical gradients
       og[j] = f2bf(d * y * sgm * (1.f + x * (1.f - sgm)));
-      ou[j] = f2bf(d * x * sgm);
+      ou[j] = f2bf(d * silu);
       sg[(8 * vec + j) * kPitch + row] = og[j];
       su[(8 * vec + j) * kPitch + row] = ou[j];
     }
