@@ -187,8 +187,15 @@ class _RopeQKV(torch.autograd.Function):
         dk = dk.contiguous() if dk is not None else z(hkv)
         dv = dv.contiguous() if dv is not None else z(hkv)
         dqkv = torch.empty(T, (hq + 2 * hkv) * d, device=dev, dtype=dt)
-        check(lib().kgwe_rope_qkv_bwd(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(cos), ptr(sin),
-                                      T, S, hq, hkv, d, stream(dqkv)), "rope_bwd")
+        if _dual_grads() and d == 128 and T % 64 == 0:
+            # also the transposed gradient, for the QKV projection's dW GEMM
+            dqkv_t = torch.empty((hq + 2 * hkv) * d, T, device=dev, dtype=dt)
+            check(lib().kgwe_rope_qkv_bwd_t(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(dqkv_t), ptr(cos),
+                                            ptr(sin), T, S, hq, hkv, d, stream(dqkv)), "rope_bwd_t")
+            _offer_transposed(dqkv, dqkv_t)
+        else:
+            check(lib().kgwe_rope_qkv_bwd(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(cos), ptr(sin),
+                                          T, S, hq, hkv, d, stream(dqkv)), "rope_bwd")
         return dqkv, None, None, None, None, None, None
 
 
