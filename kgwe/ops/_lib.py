@@ -42,8 +42,6 @@ _SIGS = {
                                   c_int64, c_int, c_int, c_int, c_int, c_void_p]),
     "kgwe_rope_qkv_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int64, c_int, c_int, c_int, c_int, c_void_p]),
-    "kgwe_rope_qkv_bwd_t": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                    c_int64, c_int, c_int, c_int, c_int, c_void_p]),
     "kgwe_cross_entropy_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                        c_int64, c_void_p]),
     "kgwe_cross_entropy_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

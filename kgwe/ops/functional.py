@@ -29,18 +29,16 @@ def _require(cond: bool, msg: str) -> None:
 # A weight gradient dW = dY^T X reduces over tokens; the library's fastest GEMM
 # layout wants dY^T and X^T (token dimension contiguous).  Transposing dY in
 # a pass of its own costs what the layout gains, so the kernel that PRODUCES
-# dY (SwiGLU backward for the gate|up projection) writes dY^T next to it and
-# offers it here, keyed by dY's storage; the linear layer's backward, the next
+# dY (SwiGLU backward for the gate|up projection; the same in the RoPE
+# backward for the QKV projection measured no gain and was dropped) writes dY^T
+# next to it and offers it here, keyed by dY's storage; the linear layer's backward, the next
 # autograd node to run, takes it.  One entry: an offer nobody took is dropped
 # by the next one.
 _offered: dict = {}
 
 
-def _dual_grads(producer: str = "") -> bool:
-    """KGWE_DUAL_GRADS: 1 (default) every producer, 0 none, or a comma list of
-    producers (swiglu, rope)."""
-    v = os.environ.get("KGWE_DUAL_GRADS", "1")
-    return v == "1" or (v != "0" and producer in v.split(","))
+def _dual_grads() -> bool:
+    return os.environ.get("KGWE_DUAL_GRADS", "1") != "0"
 
 
 def _offer_transposed(dy: torch.Tensor, dy_t: torch.Tensor) -> None:
@@ -139,7 +137,7 @@ class _SwiGLU(torch.autograd.Function):
         d2 = dout.reshape(-1, Fh).contiguous()
         dgu = torch.empty_like(gu2)
         es = gu2.element_size()
-        if _dual_grads("swiglu") and T % 64 == 0 and Fh % 64 == 0:
+        if _dual_grads() and T % 64 == 0 and Fh % 64 == 0:
             # also the transposed gradient, for the producing projection's dW GEMM
             dgu_t = torch.empty(F2, T, device=gu2.device, dtype=gu2.dtype)
             check(lib().kgwe_swiglu_bwd_t(ptr(gu2), gu2.data_ptr() + Fh * es, F2, ptr(d2),
@@ -190,15 +188,8 @@ class _RopeQKV(torch.autograd.Function):
         dk = dk.contiguous() if dk is not None else z(hkv)
         dv = dv.contiguous() if dv is not None else z(hkv)
         dqkv = torch.empty(T, (hq + 2 * hkv) * d, device=dev, dtype=dt)
-        if _dual_grads("rope") and d == 128 and T % 64 == 0:
-            # also the transposed gradient, for the QKV projection's dW GEMM
-            dqkv_t = torch.empty((hq + 2 * hkv) * d, T, device=dev, dtype=dt)
-            check(lib().kgwe_rope_qkv_bwd_t(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(dqkv_t), ptr(cos),
-                                            ptr(sin), T, S, hq, hkv, d, stream(dqkv)), "rope_bwd_t")
-            _offer_transposed(dqkv, dqkv_t)
-        else:
-            check(lib().kgwe_rope_qkv_bwd(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(cos), ptr(sin),
-                                          T, S, hq, hkv, d, stream(dqkv)), "rope_bwd")
+        check(lib().kgwe_rope_qkv_bwd(ptr(dq), ptr(dk), ptr(dv), ptr(dqkv), ptr(cos), ptr(sin),
+                                      T, S, hq, hkv, d, stream(dqkv)), "rope_bwd")
         return dqkv, None, None, None, None, None, None
 
 

@@ -93,73 +93,6 @@ __global__ __launch_bounds__(256) void rope_kernel(
   }
 }
 
-// Backward that also writes dqkv transposed: dqkvT [(Hq + 2 Hkv) * D, T], for
-// the QKV projection's weight-gradient GEMM (dW = dQKV^T X reduces over
-// tokens; with both operands token-contiguous it runs in the library's
-// fastest layout).  One workgroup = 64 token rows of one head (D = 128
-// columns), rotated as in rope_kernel<true>, written row-major, and written
-// again through an LDS transpose (pitch 72 keeps the 16-B reads aligned).
-constexpr int kRT = 64, kRPitch = 72;
-
-__global__ __launch_bounds__(256) void rope_bwd_t_kernel(
-    const bf16_t* __restrict__ src_q, const bf16_t* __restrict__ src_k, const bf16_t* __restrict__ src_v,
-    bf16_t* __restrict__ dst_qkv, bf16_t* __restrict__ dst_qkvT, const float* __restrict__ cosT,
-    const float* __restrict__ sinT, int64_t T, int S, int Hq, int Hkv) {
-  constexpr int D = 128, half = 64;
-  __shared__ __attribute__((aligned(16))) bf16_t tile[D * kRPitch];
-  const int Ht = Hq + 2 * Hkv;
-  const int head = static_cast<int>(blockIdx.x % Ht);
-  const int64_t r0 = (blockIdx.x / Ht) * static_cast<int64_t>(kRT);
-  const bf16_t* sp;
-  int hs, hl;
-  bool rotate = true;
-  if (head < Hq) {
-    sp = src_q, hs = Hq, hl = head;
-  } else if (head < Hq + Hkv) {
-    sp = src_k, hs = Hkv, hl = head - Hq;
-  } else {
-    sp = src_v, hs = Hkv, hl = head - Hq - Hkv, rotate = false;
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int s = threadIdx.x + 256 * k, row = s >> 3, c = (s & 7) * 8;
-    const int64_t r = r0 + row;
-    const bf16_t* in = sp + (r * hs + hl) * static_cast<int64_t>(D);
-    bf16_t* out = dst_qkv + r * static_cast<int64_t>(Ht) * D + static_cast<int64_t>(head) * D;
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(in + c);
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(in + half + c);
-    bf16x8 oa = a, ob = b;
-    if (rotate) {
-      const int pos = static_cast<int>(r % S);
-      const f32x4* cp = reinterpret_cast<const f32x4*>(cosT + static_cast<int64_t>(pos) * half + c);
-      const f32x4* sn = reinterpret_cast<const f32x4*>(sinT + static_cast<int64_t>(pos) * half + c);
-      const f32x4 c0 = cp[0], c1 = cp[1], s0 = sn[0], s1 = sn[1];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float cs = j < 4 ? c0[j & 3] : c1[j & 3];
-        const float sn_ = j < 4 ? s0[j & 3] : s1[j & 3];
-        const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
-        oa[j] = f2bf(x1 * cs + x2 * sn_);
-        ob[j] = f2bf(x2 * cs - x1 * sn_);
-      }
-    }
-    *reinterpret_cast<bf16x8*>(out + c) = oa;
-    *reinterpret_cast<bf16x8*>(out + half + c) = ob;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      tile[(c + j) * kRPitch + row] = oa[j];
-      tile[(half + c + j) * kRPitch + row] = ob[j];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int s = threadIdx.x + 256 * k, col = s >> 3, rv = s & 7;
-    const bf16x8 t = *reinterpret_cast<const bf16x8*>(&tile[col * kRPitch + 8 * rv]);
-    *reinterpret_cast<bf16x8*>(dst_qkvT + (static_cast<int64_t>(head) * D + col) * T + r0 + 8 * rv) = t;
-  }
-}
-
 inline int grid_for(int64_t n) {
   int64_t g = (n + 255) / 256;
   return static_cast<int>(g < 4096 ? (g < 1 ? 1 : g) : 4096);
@@ -189,19 +122,5 @@ KGWE_API int kgwe_rope_qkv_bwd(const void* dq, const void* dk, const void* dv,
                      static_cast<const bf16_t*>(dq), static_cast<const bf16_t*>(dk),
                      static_cast<const bf16_t*>(dv), nullptr, nullptr, nullptr,
                      static_cast<bf16_t*>(dqkv), cosT, sinT, T, S, Hq, Hkv, D);
-  return KGWE_CHECK_LAUNCH();
-}
-
-// As kgwe_rope_qkv_bwd, and also dqkvT [(Hq + 2 Hkv) * D, T].  D == 128 and
-// T % 64 == 0.
-KGWE_API int kgwe_rope_qkv_bwd_t(const void* dq, const void* dk, const void* dv, void* dqkv, void* dqkvT,
-                                 const float* cosT, const float* sinT, int64_t T, int S, int Hq, int Hkv, int D,
-                                 hipStream_t s) {
-  if (D != 128 || T <= 0 || T % kRT || Hq <= 0 || Hkv <= 0 || S <= 0) return -1;
-  const int64_t blocks = (T / kRT) * (Hq + 2 * Hkv);
-  if (blocks > 0x7fffffffLL) return -1;
-  hipLaunchKernelGGL(rope_bwd_t_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(dq), static_cast<const bf16_t*>(dk), static_cast<const bf16_t*>(dv),
-                     static_cast<bf16_t*>(dqkv), static_cast<bf16_t*>(dqkvT), cosT, sinT, T, S, Hq, Hkv);
   return KGWE_CHECK_LAUNCH();
 }
