@@ -96,6 +96,9 @@ def parse(argv=None):
                     help="also time the sharded-DP path with the OTHER reduce dtype for a few "
                          "steps (auto: at N > 1 on RCCL) — what halving the reduce-scatter "
                          "bytes over xGMI buys")
+    ap.add_argument("--extra-rows-timeout", type=float, default=420.0,
+                    help="N > 1: seconds the rows after the headline (busBW sweep, other reduce dtype, "
+                         "FSDP2) may take before rank 0 prints the line without them (0: no limit)")
     ap.add_argument("--in-process", action="store_true",
                     help="run as a single rank in this process (no launcher)")
     return ap.parse_args(argv)
@@ -294,6 +297,8 @@ def _release_memory() -> None:
 
 def rank_main(args) -> int:
     import faulthandler
+    import threading
+    import time
 
     faulthandler.dump_traceback_later(900, exit=False)  # stack dump if a phase hangs
     rank = int(os.environ.get("RANK", "0"))
@@ -322,14 +327,6 @@ def rank_main(args) -> int:
     if info.device.type == "cuda":
         life.start()
 
-    # Reference row "142 -> 228 GB/s" (all-reduce bus bandwidth, docs/PRD.md:117-124):
-    # RCCL over xGMI on this job's own ranks, before training allocates memory.
-    busbw = None
-    if world > 1 and not args.no_busbw:
-        from kgwe.parallel import busbw as kbus
-
-        busbw = kbus.torch_sweep(sizes=[1 << 26, 1 << 28, 1 << 30], iters=10, info=info)
-
     reduce_dtype = torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32
     tc = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
                      activation_checkpointing=args.ckpt, parallel=args.parallel,
@@ -339,67 +336,55 @@ def rank_main(args) -> int:
     attention = ("sdpa" if (args.sdpa or not attn_ops.hip_flash_available()) else "kgwe_flash_attn")
     tuned = tr.tuned_gemms
 
+    # Everything below the headline is secondary (bus-bandwidth sweep, the other
+    # reduce dtype, the FSDP2 row).  At N > 1 a watchdog bounds it: if the rows
+    # are not done in --extra-rows-timeout seconds, rank 0 prints the line with
+    # what it has and every rank exits, so a stuck secondary row can never cost
+    # the headline that was already measured.
+    extras = {"busbw": None, "reduce_row": None, "fsdp": None}
+    emit_lock = threading.Lock()
+    emitted = [False]
+
+    def bail():
+        with emit_lock:
+            if emitted[0]:
+                return
+            emitted[0] = True
+        why = {"error": f"not finished within {args.extra_rows_timeout:.0f} s (watchdog)"}
+        print(f"[bench] rank {info.rank}: secondary rows timed out, emitting the headline", file=sys.stderr,
+              flush=True)
+        if info.is_main:
+            life.stop()
+            own = [life.mean] if life.mean is not None else []
+            emit({k: (v if v is not None or k == "busbw" else why) for k, v in extras.items()}, own)
+        else:
+            time.sleep(15.0)  # rank 0 prints first
+        os._exit(0)
+
+    watchdog = None
+    if world > 1 and args.extra_rows_timeout > 0:
+        watchdog = threading.Timer(args.extra_rows_timeout, bail)
+        watchdog.daemon = True
+        watchdog.start()
+
+    # Reference row "142 -> 228 GB/s" (all-reduce bus bandwidth, docs/PRD.md:117-124):
+    # RCCL over xGMI on this job's own ranks.
+    if world > 1 and not args.no_busbw:
+        from kgwe.parallel import busbw as kbus
+
+        try:
+            extras["busbw"] = kbus.torch_sweep(sizes=[1 << 26, 1 << 28, 1 << 30], iters=10, info=info)
+        except Exception as e:  # noqa: BLE001 - reported, never faked
+            print(f"[bench] rank {info.rank}: busBW sweep failed: {e!r}", file=sys.stderr, flush=True)
+
     # Reduce-dtype row: the sharded-DP path again with the other gradient
     # reduce-scatter dtype (fp32 <-> bf16), a few steps, reported beside the
     # headline.  A failure is reported in the row, never faked.
     reduce_row = None
-    want_reduce = args.reduce_row == "on" or (args.reduce_row == "auto" and world > 1
-                                              and info.backend == "nccl")
-    if want_reduce and args.parallel == "zero":
-        other = torch.float32 if reduce_dtype == torch.bfloat16 else torch.bfloat16
-        if tr.dp is not None:
-            tr.dp.close()
-        tr = None
-        _release_memory()
-        k2, w2 = min(args.steps, 5), min(args.warmup, 2)
-        try:
-            tr3 = Trainer(TrainConfig(model=args.model, seq_len=args.seq_len,
-                                      micro_batch=args.micro_batch,
-                                      activation_checkpointing=args.ckpt, parallel="zero",
-                                      reduce_dtype=other), info)
-            a3 = argparse.Namespace(**{**vars(args), "steps": k2})
-            r3 = _row(tr3, timed_run(tr3, k2, w2), a3, info, kdist)
-            reduce_row = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r3.items()
-                          if k not in ("losses", "seconds")}
-            reduce_row.update({"grad_reduce_dtype": "bf16" if other == torch.bfloat16 else "fp32",
-                               "steps": k2, "warmup": w2})
-            tr3.dp.close()
-            del tr3
-        except Exception as e:  # noqa: BLE001 - reported, never faked
-            print(f"[bench] rank {info.rank}: reduce-dtype row failed: {e!r}", file=sys.stderr, flush=True)
-            reduce_row = {"error": repr(e)[:300]}
-            tr3 = None
-        _release_memory()
-
     fsdp = None
-    want_fsdp = args.fsdp_row == "on" or (args.fsdp_row == "auto" and world > 1)
-    if want_fsdp and args.parallel != "fsdp":
-        if tr is not None and tr.dp is not None:
-            tr.dp.close()
-        tr = None
-        _release_memory()
-        tc2 = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
-                          activation_checkpointing=args.ckpt, parallel="fsdp")
-        # A secondary row: a failure on every rank alike (out of memory, an
-        # unsupported op) is reported in the row instead of losing the
-        # headline that was already measured.
-        try:
-            tr2 = Trainer(tc2, info)
-            r2 = _row(tr2, timed_run(tr2, args.steps, min(args.warmup, 3)), args, info, kdist)
-            fsdp = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r2.items()
-                    if k not in ("losses", "seconds")}
-            del tr2
-        except Exception as e:  # noqa: BLE001 - reported, never faked
-            print(f"[bench] rank {info.rank}: FSDP row failed: {e!r}", file=sys.stderr, flush=True)
-            fsdp = {"parallelism": f"fsdp{world}", "error": repr(e)[:300]}
-            tr2 = None
-            _release_memory()
-    life.stop()
-    life_util = [u[0] for u in kdist.all_gather_floats(
-        [life.mean if life.mean is not None else -1.0], info)]
-    life_valid = [u for u in life_util if u >= 0]
 
-    if info.is_main:
+    def emit(rows: dict, life_valid: list) -> None:
+        busbw, reduce_row, fsdp = rows["busbw"], rows["reduce_row"], rows["fsdp"]
         sched = collect(sched_p, "scheduling benchmark")
         cluster = collect(cluster_p, "cluster simulation", timeout=120)
         p99 = sched["p99_ms"] if sched else None
@@ -448,6 +433,72 @@ def rank_main(args) -> int:
             "cost": meter_cost(world, tps, util),
         }
         print(json.dumps(out), flush=True)
+
+    want_reduce = args.reduce_row == "on" or (args.reduce_row == "auto" and world > 1
+                                              and info.backend == "nccl")
+    if want_reduce and args.parallel == "zero":
+        other = torch.float32 if reduce_dtype == torch.bfloat16 else torch.bfloat16
+        if tr.dp is not None:
+            tr.dp.close()
+        tr = None
+        _release_memory()
+        k2, w2 = min(args.steps, 5), min(args.warmup, 2)
+        try:
+            tr3 = Trainer(TrainConfig(model=args.model, seq_len=args.seq_len,
+                                      micro_batch=args.micro_batch,
+                                      activation_checkpointing=args.ckpt, parallel="zero",
+                                      reduce_dtype=other), info)
+            a3 = argparse.Namespace(**{**vars(args), "steps": k2})
+            r3 = _row(tr3, timed_run(tr3, k2, w2), a3, info, kdist)
+            reduce_row = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r3.items()
+                          if k not in ("losses", "seconds")}
+            reduce_row.update({"grad_reduce_dtype": "bf16" if other == torch.bfloat16 else "fp32",
+                               "steps": k2, "warmup": w2})
+            tr3.dp.close()
+            del tr3
+        except Exception as e:  # noqa: BLE001 - reported, never faked
+            print(f"[bench] rank {info.rank}: reduce-dtype row failed: {e!r}", file=sys.stderr, flush=True)
+            reduce_row = {"error": repr(e)[:300]}
+            tr3 = None
+        extras["reduce_row"] = reduce_row
+        _release_memory()
+
+    want_fsdp = args.fsdp_row == "on" or (args.fsdp_row == "auto" and world > 1)
+    if want_fsdp and args.parallel != "fsdp":
+        if tr is not None and tr.dp is not None:
+            tr.dp.close()
+        tr = None
+        _release_memory()
+        tc2 = TrainConfig(model=args.model, seq_len=args.seq_len, micro_batch=args.micro_batch,
+                          activation_checkpointing=args.ckpt, parallel="fsdp")
+        # A secondary row: a failure on every rank alike (out of memory, an
+        # unsupported op) is reported in the row instead of losing the
+        # headline that was already measured.
+        try:
+            tr2 = Trainer(tc2, info)
+            r2 = _row(tr2, timed_run(tr2, args.steps, min(args.warmup, 3)), args, info, kdist)
+            fsdp = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r2.items()
+                    if k not in ("losses", "seconds")}
+            del tr2
+        except Exception as e:  # noqa: BLE001 - reported, never faked
+            print(f"[bench] rank {info.rank}: FSDP row failed: {e!r}", file=sys.stderr, flush=True)
+            fsdp = {"parallelism": f"fsdp{world}", "error": repr(e)[:300]}
+            tr2 = None
+            _release_memory()
+        extras["fsdp"] = fsdp
+    with emit_lock:  # from here on the normal path owns the line
+        if emitted[0]:
+            time.sleep(3600)  # the watchdog is emitting and will end the process
+        emitted[0] = True
+    if watchdog is not None:
+        watchdog.cancel()
+    life.stop()
+    life_util = [u[0] for u in kdist.all_gather_floats(
+        [life.mean if life.mean is not None else -1.0], info)]
+    life_valid = [u for u in life_util if u >= 0]
+
+    if info.is_main:
+        emit(extras, life_valid)
     kdist.barrier(info)
     kdist.shutdown()
     return 0

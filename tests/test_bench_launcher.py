@@ -111,3 +111,19 @@ def test_bench_gpus1_through_launcher_on_gpu():
     assert out["steps"] == 24
     assert out["value"] is not None and out["value"] > 50.0
     assert out["util_whole_process_pct"] is not None
+
+
+def test_stuck_secondary_rows_cannot_cost_the_headline():
+    """The rows after the headline run under a watchdog at N > 1.  With a limit
+    no row can meet, rank 0 still prints exactly one line, the measured
+    headline intact and the unfinished rows marked, and the job exits 0."""
+    r, lines = _run(2, ["--model", "tiny", "--seq-len", "64", "--micro-batch", "2", "--fsdp-row", "on",
+                        "--reduce-row", "on", "--extra-rows-timeout", "0.01"], timeout=200)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ms_per_step"] > 0 and out["tokens_per_s"] > 0
+    assert len(out["loss_per_rank"]) == 2
+    assert "watchdog" in out["fsdp_row"]["error"]
+    assert "watchdog" in out["reduce_dtype_row"]["error"] or out["reduce_dtype_row"].get("grad_reduce_dtype")
+    assert "secondary rows timed out" in r.stderr
