@@ -29,6 +29,12 @@ Scale / pressure knobs:
                   nodeInfo) in the apiserver, so nodeCacheCapable=false
                   ExtenderArgs carry ~9 MB at 1,250 nodes;
   --node-cache    nodeCacheCapable=true (node names only);
+  --nodes-to-score  the profile's percentageOfNodesToScore.  The chart sets 100:
+                  the extender's verbs cost ~1 us per node, and a sampled
+                  window (kube's adaptive default: 40 % of 1,250 nodes) hides
+                  free partition slices and xGMI groups on the nodes outside
+                  it, so slice pods provision fresh partitioned GPUs instead
+                  of filling existing ones;
   --lifetime      pod lifetimes; long lifetimes fill the fleet, so pods queue
                   and high-priority pods preempt through the extender's
                   preempt verb.  Then ``sched_p99_ms`` (pods bound on their
@@ -124,7 +130,8 @@ def _apiserver_proc(conn):
     api.stop()
 
 
-def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev, ready_ev, node_cache: bool):
+def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev, ready_ev, node_cache: bool,
+                    nodes_to_score: float = 100.0):
     from ..controller.kube import KubeClient
     from ..controller.schedsim import SchedulerSim
 
@@ -141,7 +148,8 @@ def _scheduler_proc(api_url: str, ext_url: str, bound_q, stop_ev, ready_ev, node
     sys.setswitchinterval(0.0005)
     # static fleet: the node list is cached like kube-scheduler's informer
     sim = SchedulerSim(KubeClient(api_url), ext_url, on_bound=on_bound, on_preempted=on_preempted,
-                       node_cache_capable=node_cache, node_refresh_s=60.0).start()
+                       node_cache_capable=node_cache, node_refresh_s=60.0,
+                       percentage_of_nodes_to_score=nodes_to_score).start()
     ready_ev.set()
     stop_ev.wait()
     sim.stop()
@@ -250,7 +258,7 @@ def _controller_proc(conn, api_url: str, n_nodes: int, full_nodes: bool, tick_s:
 def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 50.0,
         lifetime_s: tuple = (0.5, 3.0), seed: int = 7, timeout_s: float = 300.0,
         tick_s: float = 1.0, reclaim_idle_s: float = 2.0, full_nodes: bool = False,
-        node_cache: bool = False) -> dict:
+        node_cache: bool = False, nodes_to_score: float = 100.0) -> dict:
     from ..controller.kube import KubeClient
     from ..core import LatencyHistogram
 
@@ -275,7 +283,8 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
 
     bound_q = ctx.Queue()
     stop_ev, ready_ev = ctx.Event(), ctx.Event()
-    sch_p = ctx.Process(target=_scheduler_proc, args=(api_url, ext_url, bound_q, stop_ev, ready_ev, node_cache),
+    sch_p = ctx.Process(target=_scheduler_proc, args=(api_url, ext_url, bound_q, stop_ev, ready_ev, node_cache,
+                              nodes_to_score),
                         daemon=True)
     sch_p.start()
     ready_ev.wait(timeout=120)  # node cache synced
@@ -388,6 +397,8 @@ def run(n_pods: int = 2000, job_gpus: int = 8, n_nodes: int = 64, rate: float = 
         "arrival_rate_per_s": rate, "lifetime_s": list(lifetime_s),
         "node_objects": "full (~7 KB each)" if full_nodes else "minimal",
         "node_cache_capable": node_cache,
+        # the kgwe-scheduler profile's percentageOfNodesToScore (0: kube's adaptive default)
+        "percentage_of_nodes_to_score": nodes_to_score,
         # pods bound on their FIRST scheduling cycle: the scheduler's own latency
         "sched_p50_ms": round(first_hist.quantile_ms(0.50), 3),
         "sched_p99_ms": round(first_hist.quantile_ms(0.99), 3),
@@ -422,6 +433,9 @@ def main(argv=None) -> int:
     ap.add_argument("--lifetime", default="0.5,3.0", help="min,max pod lifetime seconds")
     ap.add_argument("--full-nodes", action="store_true")
     ap.add_argument("--node-cache", action="store_true", help="nodeCacheCapable=true (names only)")
+    ap.add_argument("--nodes-to-score", type=float, default=100.0,
+                    help="the profile's percentageOfNodesToScore (chart default 100; 0 = kube-scheduler's "
+                         "adaptive default, 40 %% of 1,250 nodes)")
     ap.add_argument("--timeout", type=float, default=300.0)
     ap.add_argument("--then-nodes", type=int, default=0,
                     help="afterwards run the same load on a fleet of this many nodes "
@@ -430,11 +444,13 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     lo, hi = (float(x) for x in a.lifetime.split(","))
     res = run(n_pods=a.pods, job_gpus=a.job_gpus, n_nodes=a.nodes, rate=a.rate, lifetime_s=(lo, hi),
-              full_nodes=a.full_nodes, node_cache=a.node_cache, timeout_s=a.timeout)
+              full_nodes=a.full_nodes, node_cache=a.node_cache, timeout_s=a.timeout,
+              nodes_to_score=a.nodes_to_score)
     if a.then_nodes:
         res[f"fleet_{a.then_nodes}_nodes"] = run(
             n_pods=a.pods, job_gpus=a.job_gpus, n_nodes=a.then_nodes, rate=a.rate, lifetime_s=(lo, hi),
-            full_nodes=a.full_nodes, node_cache=a.node_cache, timeout_s=a.timeout)
+            full_nodes=a.full_nodes, node_cache=a.node_cache, timeout_s=a.timeout,
+            nodes_to_score=a.nodes_to_score)
     print(json.dumps(res) if a.json else json.dumps(res, indent=1), flush=True)
     os._exit(0)  # reaper timers / daemon threads: do not wait for them
 

@@ -70,7 +70,7 @@ class SchedulerSim:
     def __init__(self, kube: KubeClient, extender_url: str, bind_workers: int = 4,
                  on_bound=None, on_failed=None, initial_backoff_s: float = 1.0,
                  max_backoff_s: float = 10.0, node_cache_capable: bool = False, preempt: bool = True,
-                 on_preempted=None, node_refresh_s: float = 1.0, adaptive_nodes_to_score: bool = True,
+                 on_preempted=None, node_refresh_s: float = 1.0, percentage_of_nodes_to_score: float = 0.0,
                  max_bind_threads: int = 256):
         self.kube = kube
         self.ext = _Http(extender_url)
@@ -83,7 +83,8 @@ class SchedulerSim:
         self._bind_lock = threading.Lock()
         self.node_cache_capable = node_cache_capable
         self.node_refresh_s = node_refresh_s  # unused: the node cache follows a watch (see _informer)
-        self.adaptive = adaptive_nodes_to_score
+        # the profile's percentageOfNodesToScore; 0 = kube-scheduler's adaptive default
+        self.pct_to_score = float(percentage_of_nodes_to_score)
         self._start = 0  # kube-scheduler's rotating start index over the node list
         self.preempt = preempt
         self._node_json: dict[str, bytes] = {}
@@ -276,15 +277,16 @@ class SchedulerSim:
             self._rt["cycle"].append(time.perf_counter() - t_cycle)
 
     def _candidates(self, names: list) -> list:
-        """kube-scheduler's percentageOfNodesToScore (adaptive default): it
-        stops searching after max(100, N * max(5, 50 - N / 125) %) feasible
-        nodes, starting where the previous cycle stopped, and only those reach
-        the extender.  (Its own plugins would also drop full nodes; the
-        extender filter covers that here.)"""
+        """kube-scheduler's percentageOfNodesToScore: it stops searching after
+        max(100, N * pct %) feasible nodes, starting where the previous cycle
+        stopped, and only those reach the extender.  pct is the profile's
+        setting, or with 0 the adaptive default max(5, 50 - N / 125); at 100
+        every node is a candidate.  (Its own plugins would also drop full
+        nodes; the extender filter covers that here.)"""
         n = len(names)
-        if not self.adaptive or n <= 100:
+        if n <= 100 or self.pct_to_score >= 100.0:
             return names
-        pct = max(5.0, 50.0 - n / 125.0)
+        pct = self.pct_to_score if self.pct_to_score > 0 else max(5.0, 50.0 - n / 125.0)
         k = min(n, max(100, int(n * pct / 100.0)))
         start = self._start % n
         self._start = start + k

@@ -20,7 +20,7 @@
 #   ops                   tools/ops_bench.py (every hand-written op against its roofline)
 #   infer N [args]        co-location bench with N clients (kgwe.bench.infer colocate)
 #   sched [args]          extender latency bench (kgwe.bench.sched_latency)
-#   sched-suite           the seven latency / pressure runs reported under profiles/*_sched/
+#   sched-suite           the eight latency / pressure runs reported under profiles/*_sched/
 #   probe-pmc             counter validation of the HBM / LDS probe kernels
 #   ab VAR=VALUE [bench args]
 #                         the training bench with VAR=VALUE set, then without, twice over, on
@@ -134,6 +134,7 @@ sched-suite)
     python tools/sched_brief.py "gpurun_out/sched/$name.json"
   }
   one scale_1250n_names_50pps   --pods 3000 --nodes 1250 --rate 50 --node-cache
+  one scale_1250n_names_50pps_sampled --pods 3000 --nodes 1250 --rate 50 --node-cache --nodes-to-score 0
   one scale_1250n_names_100pps  --pods 5000 --nodes 1250 --rate 100 --node-cache
   one scale_1250n_full_10pps    --pods 600 --nodes 1250 --rate 10 --full-nodes
   one scale_64n_names_50pps     --pods 2000 --nodes 64 --rate 50 --node-cache
