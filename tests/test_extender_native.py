@@ -323,3 +323,22 @@ def test_preempt_verb_names_only_victims_on_the_node_and_hands_peers_to_release(
     rel = plat.release(by_node["n0"])
     assert rel["evict_gang_peers"] == [by_node["n1"]]
     assert "evict_gang_peers" not in plat.release(by_node["n1"])
+
+
+def test_standin_candidate_window_follows_the_profile_setting():
+    """percentageOfNodesToScore: 100 hands every node to the extender; 0 is
+    kube-scheduler's adaptive default (a rotating window of max(100, N * (50 -
+    N / 125) %) nodes); an explicit value is taken as given."""
+    from kgwe.controller.schedsim import SchedulerSim
+
+    names = [f"n{i}" for i in range(1250)]
+    every = SchedulerSim(None, "http://127.0.0.1:1", percentage_of_nodes_to_score=100)
+    assert every._candidates(names) == names
+    adaptive = SchedulerSim(None, "http://127.0.0.1:1")
+    first, second = adaptive._candidates(names), adaptive._candidates(names)
+    assert len(first) == 500 and first[0] == "n0" and second[0] == "n500"
+    third = adaptive._candidates(names)  # wraps round the node list
+    assert third[0] == "n1000" and third[-1] == "n249"
+    ten = SchedulerSim(None, "http://127.0.0.1:1", percentage_of_nodes_to_score=10)
+    assert len(ten._candidates(names)) == 125
+    assert len(ten._candidates(names[:90])) == 90  # small fleets are never sampled
