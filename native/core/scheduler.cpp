@@ -1145,13 +1145,19 @@ NodeScore Scheduler::score_node(const NodeTopology& n, const WorkloadRequest& w)
       return used_on[gpu_of[a]] > used_on[gpu_of[b]];
     });
     for (int i = 0; i < w.partition_count; ++i) s.partitions.push_back(parts[order[i]]->id);
-    int total_slices = 0, used_slices = 0;
-    for (auto& kv : used_on) used_slices += kv.second;
-    for (const auto& g : n.gpus)
-      if (g.partition.compute == w.partition_mode) total_slices += static_cast<int>(g.partition.instances.size());
+    // Best fit across the fleet: the score is how full the GPU that takes the
+    // (first) slice is afterwards, so slice pods fill the fullest partitioned
+    // GPU anywhere and the emptiest ones drain and go back to SPX.  Slices on
+    // an existing partition take no whole GPU from the node, so the node's
+    // whole-GPU balance does not enter.
+    const std::string& target = gpu_of[order[0]];
+    int on_target = 0, target_slices = 0;
+    for (int i = 0; i < w.partition_count; ++i) on_target += gpu_of[order[i]] == target;
+    if (const GpuDevice* tg = n.gpu(target)) target_slices = static_cast<int>(tg->partition.instances.size());
+    const int fullness = target_slices ? 100 * (used_on[target] + on_target) / target_slices : 0;
     s.topology = 100;
-    s.resource = 50 + (total_slices ? 50 * used_slices / total_slices : 0);  // packing
-    s.balance = balance_score(n, 0);
+    s.resource = std::min(100, fullness);
+    s.balance = s.resource;
   } else {
     auto avail = free_gpus(n, w);
     if (static_cast<int>(avail.size()) < w.gpu_count) return s;

@@ -155,3 +155,36 @@ def test_memory_mode_requests_cpx_nps2():
     ops = p.reclaim_idle_partitions()
     assert ops and all(o["to"] == "SPX" and o["memory_to"] == "NPS1" for o in ops)
     assert all(g["partition"]["memory"] == "NPS1" for g in p.node("n0")["gpus"])
+
+
+def test_slice_pods_fill_the_fullest_partitioned_gpu_in_the_fleet():
+    """Best fit across nodes is by the GPU that takes the slice: a slice pod
+    scores the node whose CPX GPU is fuller higher, whatever the nodes' whole
+    GPUs are doing, so the emptier partitioned GPU drains and can go back to
+    SPX."""
+    p = Platform({})
+    for n in ("na", "nb"):
+        p.add_fake_node(make_fixture(n, 8, 2))
+
+    def on(node, uid, wl):
+        wl = {**wl, "spec": {**wl["spec"], "nodeSelector": {"kubernetes.io/hostname": node}}}
+        d = p.schedule(wl)
+        assert d["ok"] and d["node"] == node, d
+        return d
+
+    p.ensure_partitions("CPX", 16)                  # one CPX GPU on each node (bin-packed per node)
+    modes = {n: [g["partition"]["compute"] for g in p.node(n)["gpus"]].count("CPX") for n in ("na", "nb")}
+    if modes != {"na": 1, "nb": 1}:
+        pytest.skip(f"fixture partitions landed as {modes}")
+    for i in range(6):
+        on("na", f"a{i}", part_wl(f"a{i}"))         # na's CPX GPU: 6 of 8 in use
+    for i in range(2):
+        on("nb", f"b{i}", part_wl(f"b{i}"))         # nb's: 2 of 8
+    # nb is the busier node by whole GPUs
+    on("nb", "train", {"metadata": {"name": "train", "uid": "train"},
+                       "spec": {"gpuRequirements": {"count": 6}}})
+    sa, sb = p.score_node("na", part_wl("x")), p.score_node("nb", part_wl("x"))
+    assert sa["total"] > sb["total"], (sa, sb)
+    assert sa["resource"] == 100 * 7 // 8 and sb["resource"] == 100 * 3 // 8
+    d = p.schedule(part_wl("x"))
+    assert d["ok"] and d["node"] == "na"
