@@ -17,6 +17,7 @@
 #                         rocprofv3 kernel trace + stats of a python program
 #   wgrad [bench args]    weight-gradient GEMM: numerics, then tools/wgrad_kernel_bench.py
 #   attn                  attention numerics, then tools/attn_bench.py
+#   attn-modes M...       forward attention kernel variants: numerics tests + timing per KGWE_FA_FWD mode
 #   ops                   tools/ops_bench.py (every hand-written op against its roofline)
 #   infer N [args]        co-location bench with N clients (kgwe.bench.infer colocate)
 #   sched [args]          extender latency bench (kgwe.bench.sched_latency)
@@ -101,6 +102,16 @@ attn)
   tail -3 gpurun_out/attn_test.log
   run 200 gpurun_out/attn_bench.log python tools/attn_bench.py
   grep -v amdgpu.ids gpurun_out/attn_bench.log | tail -8 ;;
+attn-modes)
+  # forward kernel variants (KGWE_FA_FWD, read once per process): numerics, then timing
+  for mode in "$@"; do
+    export KGWE_FA_FWD=$mode
+    echo "== KGWE_FA_FWD=$mode"
+    run 300 "gpurun_out/attn_test_m$mode.log" $PYTEST tests/test_flash_attn_gpu.py -x
+    tail -1 "gpurun_out/attn_test_m$mode.log"
+    run 200 "gpurun_out/attn_modes_m$mode.log" python tools/attn_fwd_modes.py
+    grep "^mode" "gpurun_out/attn_modes_m$mode.log"
+  done ;;
 ops)
   run 400 gpurun_out/ops_bench.log python tools/ops_bench.py "$@"
   cat gpurun_out/ops_bench.log ;;
