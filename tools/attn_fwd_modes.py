@@ -1,6 +1,8 @@
-"""Time the flash-attention forward of the mode in KGWE_FA_FWD (read once per
-process by the launcher: 0 lock-step kernel, 1 / 2 phase-skewed halves, 3 the
-skewed kernel's code with nobody late) and compare it with PyTorch SDPA."""
+"""Time the flash-attention forward at the training shapes (B = 2 / 4, causal
+and full) and compare it with PyTorch SDPA.  With the variant kernel of
+profiles/r03_attn/skew_kernel.patch applied, KGWE_FA_FWD (read once per process
+by the launcher) selects it: 0 shipped kernel, 1 / 2 phase-skewed halves, 3 the
+variant's code with nobody late; without the patch the variable does nothing."""
 import os
 import sys
 import time

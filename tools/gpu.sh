@@ -17,7 +17,8 @@
 #                         rocprofv3 kernel trace + stats of a python program
 #   wgrad [bench args]    weight-gradient GEMM: numerics, then tools/wgrad_kernel_bench.py
 #   attn                  attention numerics, then tools/attn_bench.py
-#   attn-modes M...       forward attention kernel variants: numerics tests + timing per KGWE_FA_FWD mode
+#   attn-modes M...       forward attention: numerics tests + timing at B = 2 / 4, once per KGWE_FA_FWD value
+#                         (selects a kernel only with profiles/r03_attn/skew_kernel.patch applied; plain: attn-modes 0)
 #   ops                   tools/ops_bench.py (every hand-written op against its roofline)
 #   infer N [args]        co-location bench with N clients (kgwe.bench.infer colocate)
 #   sched [args]          extender latency bench (kgwe.bench.sched_latency)
