@@ -78,7 +78,9 @@ prof)
     python3 bench.py --in-process --steps 2 --warmup 1 --no-sched --no-cluster "$@"
   f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
   python3 tools/prof_summary.py "$f" gpurun_out/prof/summary --title "bench.py training step (2 steps)" --steps 2 \
-    && head -45 gpurun_out/prof/summary/SUMMARY.md ;;
+    && head -45 gpurun_out/prof/summary/SUMMARY.md
+  t=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
+  python3 tools/step_table.py "$t" > gpurun_out/prof/summary/step_table.md && cat gpurun_out/prof/summary/step_table.md ;;
 pmc)
   out=gpurun_out/${1:?out dir}; counters=${2:?counters}; shift 2; [ "$1" = "--" ] && shift
   rocprof_env; rm -rf "$out"; mkdir -p "$out"
