@@ -58,7 +58,7 @@ class Generator:
                       and dec.gemv_supported(batch, c.dim) and dec.gemv_supported(batch, hq * d))
         if self.fused:
             self.hbuf = torch.empty(2, batch, c.dim, device=self.dev, dtype=p.dtype)
-            self.best = torch.zeros(batch, dec.argmax_slots(c.vocab_size), dtype=torch.long, device=self.dev)
+            self.best = torch.zeros(batch, dec.argmax_slots(c.vocab_size, batch), dtype=torch.long, device=self.dev)
             self.w2_fused = dec.gemv_supported(batch, c.ffn_dim)
 
     # ------------------------------------------------------------ prefill

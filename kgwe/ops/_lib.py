@@ -62,6 +62,12 @@ _SIGS = {
                                  c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "kgwe_decode_argmax_finish": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "kgwe_decode_argmax_slots": (c_int, [c_int, c_int, c_int]),
+    "kgwe_decode_skinny": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "kgwe_decode_skinny_workspace": (c_int64, [c_int, c_int, c_int, c_int]),
+    "kgwe_decode_skinny_blocks": (c_int, [c_int]),
+    "kgwe_decode_skinny_slices": (c_int, [c_int, c_int, c_int]),
+    "kgwe_decode_skinny_max_m": (c_int, []),
     "kgwe_adamw_tensor_bytes": (c_int, []),
     "kgwe_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                 c_int, c_int, c_int, c_int, c_void_p]),

@@ -5,9 +5,11 @@
 * ``decode_attention`` — split-K GQA attention of one query token per
   sequence over the cache (HBM-bound; one workgroup per (sequence, kv head,
   key chunk) serves all query heads of the group);
-* ``gemv`` — the decode step's projections (M <= 8 rows) as weight-streaming
-  skinny GEMMs (``native/ops/gemv.hip``) with the layer's RMSNorm (+ residual
-  add), SwiGLU and greedy argmax fused in.
+* ``gemv`` — the decode step's projections as weight-streaming skinny GEMMs
+  with the layer's RMSNorm (+ residual add), SwiGLU and greedy argmax fused
+  in: M <= 8 rows on the vector ALU (``native/ops/gemv.hip``), 8 < M <= 32 —
+  the batch of a shared-model server — on the matrix cores
+  (``native/ops/skinny_gemm.hip``).
 
 On a GPU the HIP kernels are mandatory; on CPU the fp32 references below run
 (also the numerics oracle of the GPU tests).
@@ -141,9 +143,17 @@ class DecodeAttention:
 # ------------------------------------------------------------------ projections
 GEMV_PLAIN, GEMV_NORM, GEMV_SWIGLU, GEMV_NORM_SWIGLU, GEMV_NORM_ARGMAX = 0, 1, 2, 3, 5
 GEMV_M = (1, 2, 4, 8)
+SKINNY_MAX_M = 32
+
+
+def _skinny(M: int) -> bool:
+    """Batches past the vector-ALU kernels' 8 rows go to the MFMA kernel."""
+    return 8 < M <= SKINNY_MAX_M
 
 
 def gemv_supported(M: int, K: int) -> bool:
+    if _skinny(M):
+        return K % 64 == 0
     return M in GEMV_M and K % 8 == 0 and M * K * 2 <= 96 * 1024
 
 
@@ -198,11 +208,31 @@ def max_wgs() -> int:
     return _MAX_WGS
 
 
-def argmax_slots(N: int) -> int:
+def argmax_slots(N: int, M: int = 1) -> int:
     """Entries per row of the ARGMAX partial-maximum buffer for an [N, K] head
-    (one per workgroup of the capped grid)."""
+    at batch M (one per workgroup of the capped grid; one per block of 32
+    weight rows for 8 < M <= 32)."""
+    if _skinny(M):
+        return (N + 31) // 32
     R = _rows_per_wave(N)
     return min((N + 4 * R - 1) // (4 * R), max_wgs())
+
+
+_SKINNY_WS: dict = {}
+
+
+def _skinny_workspace(x: torch.Tensor, N: int, K: int, swiglu: bool) -> torch.Tensor:
+    """Split-K partials + tickets of the MFMA kernel for this shape, zeroed
+    once (every launch leaves the tickets at zero), one per stream: launches
+    that share it are ordered by the stream."""
+    cus = max_wgs() // 8
+    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream, N, K, swiglu, cus)
+    ws = _SKINNY_WS.get(key)
+    if ws is None:
+        nbytes = lib().kgwe_decode_skinny_workspace(N, K, int(swiglu), cus)
+        _require(nbytes > 0, "gemv: unsupported [N, K] for the batched decode kernel")
+        ws = _SKINNY_WS[key] = torch.zeros((nbytes + 3) // 4, dtype=torch.int32, device=x.device)
+    return ws
 
 
 def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=None, eps: float = 1e-5,
@@ -225,16 +255,25 @@ def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=N
     M, K = x.shape
     N = w.shape[0] // 2 if mode & GEMV_SWIGLU else w.shape[0]
     _require(x.dtype == w.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()
-             and w.shape[1] == K and gemv_supported(M, K), "gemv: bf16 contiguous x [M<=8, K%8==0], w [N, K]")
+             and w.shape[1] == K and gemv_supported(M, K), "gemv: bf16 contiguous x [M in 1,2,4,8 (K%8==0) or 9..32 (K%64==0)], w [N, K]")
     _require(not (mode & GEMV_NORM) or (g is not None and g.numel() == K), "gemv: NORM needs g [K]")
     _require(res is None or (res.shape == x.shape and res.is_contiguous()), "gemv: res must match x")
     _require(h_out is None or (h_out.shape == x.shape and h_out.data_ptr() not in (
         x.data_ptr(), res.data_ptr() if res is not None else -1)), "gemv: h_out must not alias x / res")
     _require(mode != GEMV_NORM_ARGMAX or (best is not None and best.dtype == torch.long
-                                          and best.numel() == M * argmax_slots(N)),
-             "gemv: ARGMAX needs best int64 [M, argmax_slots(N)]")
+                                          and best.numel() == M * argmax_slots(N, M)),
+             "gemv: ARGMAX needs best int64 [M, argmax_slots(N, M)]")
     if y is None and mode != GEMV_NORM_ARGMAX:
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    if _skinny(M):
+        ws = _skinny_workspace(x, N, K, bool(mode & GEMV_SWIGLU))
+        check(lib().kgwe_decode_skinny(ptr(x), ptr(res) if res is not None else None,
+                                       ptr(g) if g is not None else None,
+                                       ptr(h_out) if h_out is not None else None, float(eps), ptr(w),
+                                       ptr(y) if y is not None else None,
+                                       ptr(best) if best is not None else None, ptr(ws), M, N, K, mode,
+                                       max_wgs() // 8, stream(x)), "decode_skinny")
+        return y
     check(lib().kgwe_decode_gemv(ptr(x), ptr(res) if res is not None else None,
                                  ptr(g) if g is not None else None,
                                  ptr(h_out) if h_out is not None else None, float(eps), ptr(w),

@@ -348,7 +348,7 @@ KGWE_API int kgwe_decode_argmax_slots(int N, int rows_per_wave, int max_wgs) {
 
 KGWE_API int kgwe_decode_argmax_finish(const unsigned long long* best, long long* tok, int M, int slots,
                                        hipStream_t s) {
-  if (M <= 0 || M > kMaxM || slots <= 0) return -1;
+  if (M <= 0 || M > 64 || slots <= 0) return -1;  // one workgroup per batch row (gemv: <= 8, skinny_gemm: <= 32)
   hipLaunchKernelGGL(argmax_finish_kernel, dim3(M), dim3(kFinishThreads), 0, s, best, tok, slots);
   return KGWE_CHECK_LAUNCH();
 }

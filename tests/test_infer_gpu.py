@@ -94,6 +94,9 @@ def test_fused_rope_attention_matches_separate_kernels(B, hq, hkv, d, smax, lens
 @pytest.mark.parametrize("M,N,K,mode", [
     (1, 384, 2048, 0), (4, 3072, 2048, 1), (8, 520, 2048, 1), (4, 2048, 8192, 0),
     (2, 1024, 2048, 3), (4, 4096, 2048, 3), (4, 20000, 2048, 1), (4, 96, 64, 2),
+    # 8 < M <= 32: the matrix-core kernel (one K slice; K split over workgroups; ragged N and M)
+    (32, 3072, 2048, 1), (32, 2048, 8192, 0), (12, 520, 2048, 1), (32, 8192, 2048, 3), (17, 1000, 4096, 3),
+    (32, 96, 64, 2), (9, 20000, 2048, 1), (32, 4096, 14336, 0),
 ])
 def test_gemv_modes_match_fp32_reference(M, N, K, mode):
     from kgwe.ops import decode as dec
@@ -115,36 +118,38 @@ def test_gemv_modes_match_fp32_reference(M, N, K, mode):
         assert torch.equal(h_out.cpu(), hr)
 
 
-def test_gemv_argmax_matches_torch_argmax():
+@pytest.mark.parametrize("M,N,K", [(4, 50000, 2048), (32, 50000, 2048), (13, 50001, 4096)])
+def test_gemv_argmax_matches_torch_argmax(M, N, K):
     from kgwe.ops import decode as dec
 
     g = torch.Generator(device="cuda").manual_seed(4)
-    M, N, K = 4, 50000, 2048
     x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     w[123] = w[77]  # an exact tie: the first index must win, as in torch.argmax
     gw = torch.ones(K, device="cuda", dtype=torch.bfloat16)
-    best = torch.zeros(M, dec.argmax_slots(N), dtype=torch.long, device="cuda")
+    best = torch.zeros(M, dec.argmax_slots(N, M), dtype=torch.long, device="cuda")
     tok = torch.empty(M, dtype=torch.long, device="cuda")
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    for _ in range(2):  # a second step overwrites every partial
+    for _ in range(2):  # a second step overwrites every partial (and finds the split-K tickets at zero)
         dec.gemv(x, w, dec.GEMV_NORM_ARGMAX, g=gw, y=y, best=best)
         dec.argmax_finish(best, tok)
         torch.cuda.synchronize()
         assert torch.equal(tok, y.argmax(-1)), (tok, y.argmax(-1))
 
 
-@pytest.mark.parametrize("preset", ["tiny", "llama3.2-1b"])
-def test_graph_decode_logits_match_full_forward(preset):
+@pytest.mark.parametrize("preset,batch", [("tiny", 2), ("llama3.2-1b", 2), ("tiny", 12), ("llama3.2-1b", 32)])
+def test_graph_decode_logits_match_full_forward(preset, batch):
+    """batch <= 8: the vector-ALU projections; 8 < batch <= 32: the matrix-core
+    ones (a serving batch).  Six graph replays, each checked."""
     from kgwe.models import llama
     from kgwe.models.infer import Generator
 
     torch.manual_seed(0)
     m = llama.build(preset, device="cuda", dtype=torch.bfloat16)
     m.eval()
-    gen = Generator(m, batch=2, max_seq=96, keep_logits=True)
-    assert gen.fused  # the fused GEMV decode path is the one under test
-    prompt = torch.randint(0, m.cfg.vocab_size, (2, 40), device="cuda")
+    gen = Generator(m, batch=batch, max_seq=96, keep_logits=True)
+    assert gen.fused  # the fused decode path is the one under test
+    prompt = torch.randint(0, m.cfg.vocab_size, (batch, 40), device="cuda")
     gen.prefill(prompt)
     gen.capture()
     seq = [prompt]
