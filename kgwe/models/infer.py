@@ -60,6 +60,7 @@ class Generator:
             self.hbuf = torch.empty(2, batch, c.dim, device=self.dev, dtype=p.dtype)
             self.best = torch.zeros(batch, dec.argmax_slots(c.vocab_size, batch), dtype=torch.long, device=self.dev)
             self.w2_fused = dec.gemv_supported(batch, c.ffn_dim)
+            self.split_norm = batch > 8
 
     # ------------------------------------------------------------ prefill
     @torch.no_grad()
@@ -106,7 +107,8 @@ class Generator:
     # ------------------------------------------------------------ decode
     @torch.no_grad()
     def _step_fused(self) -> None:
-        """One decode step in 5 kernels per layer: [RMSNorm(+res) -> wqkv],
+        """One decode step in 5 kernels per layer (7 for a serving batch, whose
+        two RMSNorms are kernels of their own): [RMSNorm(+res) -> wqkv],
         [RoPE + KV append + split-K attention + merge], wo,
         [RMSNorm(+res) -> w13 -> SwiGLU], w2; and [RMSNorm(+res) -> LM head ->
         argmax] at the end."""
@@ -115,6 +117,28 @@ class Generator:
         B, eps = self.B, c.norm_eps
         x = m.tok_embeddings(self.tok)  # [B, dim]
         res = None
+        if self.split_norm:
+            # A serving batch (8 < B <= 32): the projections run on the matrix-core
+            # kernel, whose every workgroup stages x.  Fused, each of them would redo
+            # the RMSNorm of all B rows; one small kernel does it once instead, and
+            # the projections stage a plain copy.  SwiGLU and argmax stay fused.
+            for i, layer in enumerate(m.layers):
+                at, ff = layer.attention, layer.feed_forward
+                xn, h = K.rmsnorm(x, layer.attention_norm, eps, residual=res)
+                qkv = dec.gemv(xn, at.wqkv)
+                o = self.attn.rope_attend(qkv, self.cos, self.sin, self.kv[0, i], self.kv[1, i], self.lens)
+                a = dec.gemv(o.view(B, -1), at.wo)
+                xn, res = K.rmsnorm(a, layer.ffn_norm, eps, residual=h)
+                f = dec.gemv(xn, ff.w13, dec.GEMV_SWIGLU)
+                x = dec.gemv(f, ff.w2) if self.w2_fused else K.linear(f, ff.w2)
+            xn, _ = K.rmsnorm(x, m.norm, eps, residual=res)
+            if self.keep_logits and self.logits is None:
+                self.logits = torch.empty(B, c.vocab_size, device=self.dev, dtype=x.dtype)
+            dec.gemv(xn, m.output, dec.GEMV_ARGMAX, y=self.logits if self.keep_logits else None, best=self.best)
+            dec.argmax_finish(self.best, self.tok)
+            self.pos.add_(self.active)
+            self.lens.add_(self.active)
+            return
         hA, hB = self.hbuf[0], self.hbuf[1]
         for i, layer in enumerate(m.layers):
             at, ff = layer.attention, layer.feed_forward

@@ -97,6 +97,11 @@ class DecodeAttention:
             _require(hq % hkv == 0 and hq // hkv in (1, 2, 4, 8) and d in (64, 128),
                      "decode_attention: head_dim 64/128 and Hq/Hkv in {1,2,4,8}")
             self.splits = int(lib().kgwe_decode_attn_splits(B, hkv, smax))
+            import os  # noqa: PLC0415
+
+            forced = int(os.environ.get("KGWE_DECODE_SPLITS", "0"))  # tuning knob: 1..64
+            if forced > 0:
+                self.splits = max(1, min(64, forced, (smax + 63) // 64))
             n = int(lib().kgwe_decode_attn_workspace(B, hq, d, self.splits))
             # zeroed once: the tail holds the split tickets, which every call
             # returns to zero
@@ -142,6 +147,7 @@ class DecodeAttention:
 
 # ------------------------------------------------------------------ projections
 GEMV_PLAIN, GEMV_NORM, GEMV_SWIGLU, GEMV_NORM_SWIGLU, GEMV_NORM_ARGMAX = 0, 1, 2, 3, 5
+GEMV_ARGMAX = 4  # argmax of a projection whose input is already normalised (8 < M <= 32 only)
 GEMV_M = (1, 2, 4, 8)
 SKINNY_MAX_M = 32
 
@@ -245,7 +251,7 @@ def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=N
         yy, h = gemv_reference(x, w, mode, res, g, eps)
         if h_out is not None and res is not None and mode & GEMV_NORM:
             h_out.copy_(h)
-        if mode == GEMV_NORM_ARGMAX and best is not None:
+        if mode & GEMV_ARGMAX and best is not None:
             best.zero_()
             best[:, 0] = yy.float().argmax(-1)  # CPU: the token itself in slot 0
         if y is not None:
@@ -260,10 +266,11 @@ def gemv(x: torch.Tensor, w: torch.Tensor, mode: int = GEMV_PLAIN, res=None, g=N
     _require(res is None or (res.shape == x.shape and res.is_contiguous()), "gemv: res must match x")
     _require(h_out is None or (h_out.shape == x.shape and h_out.data_ptr() not in (
         x.data_ptr(), res.data_ptr() if res is not None else -1)), "gemv: h_out must not alias x / res")
-    _require(mode != GEMV_NORM_ARGMAX or (best is not None and best.dtype == torch.long
+    _require(mode != GEMV_ARGMAX or _skinny(M), "gemv: ARGMAX without NORM needs 8 < M <= 32")
+    _require(not mode & GEMV_ARGMAX or (best is not None and best.dtype == torch.long
                                           and best.numel() == M * argmax_slots(N, M)),
              "gemv: ARGMAX needs best int64 [M, argmax_slots(N, M)]")
-    if y is None and mode != GEMV_NORM_ARGMAX:
+    if y is None and not mode & GEMV_ARGMAX:
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
     if _skinny(M):
         ws = _skinny_workspace(x, N, K, bool(mode & GEMV_SWIGLU))

@@ -307,7 +307,9 @@ KGWE_API int64_t kgwe_decode_attn_workspace(int B, int Hq, int D, int splits) {
 // Split count for a cache of Smax keys: enough workgroups to cover the 256
 // CUs about twice, at least 64 keys per split.
 KGWE_API int kgwe_decode_attn_splits(int B, int Hkv, int Smax) {
-  const int want = (512 + B * Hkv - 1) / (B * Hkv);
+  // ~1024 workgroups: at a serving batch (B = 32, 8 kv heads) 4 splits measured 23.0 us per
+  // layer against 31.8 with 2 and 25.8 with 8 (640 of 1,024 positions cached)
+  const int want = (1024 + B * Hkv - 1) / (B * Hkv);
   const int most = (Smax + 63) / 64;
   return std::max(1, std::min({want, most, 64}));  // the merge holds one split per lane
 }

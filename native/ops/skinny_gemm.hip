@@ -52,7 +52,7 @@ constexpr int kMaxSlice = 2048;  // K columns staged per workgroup
 constexpr int kU = 8;            // k-steps (16 columns each) in flight per wave
 constexpr int kTile = kNB * kMB;  // fp32 values of one accumulator tile
 
-enum Mode { kPlain = 0, kNorm = 1, kSwiglu = 2, kNormSwiglu = 3, kNormArgmax = 5 };
+enum Mode { kPlain = 0, kNorm = 1, kSwiglu = 2, kNormSwiglu = 3, kArgmax = 4, kNormArgmax = 5 };
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(mfma8, a), __builtin_bit_cast(mfma8, b), c,
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kT) void skinny_kernel(
     int N, int K, int KS, int NB) {
   constexpr bool NORM = (MODE & kNorm) != 0;
   constexpr bool SWIGLU = (MODE & kSwiglu) != 0;
-  constexpr bool ARGMAX = MODE == kNormArgmax;
+  constexpr bool ARGMAX = (MODE & kArgmax) != 0;
   constexpr int TILES = SWIGLU ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];  // [kMB][Ks + 8]
   // cross-wave hand-off: [0], [1] waves 2, 3 -> 0, 1; [2] wave 1 -> 0 (a buffer of its own: wave 0 may
@@ -101,36 +101,94 @@ __global__ __launch_bounds__(kT) void skinny_kernel(
   const int k0 = ks * Ks;
   const int nb0 = static_cast<int>(blockIdx.x) / KS, nb_step = static_cast<int>(gridDim.x) / KS;
 
-  // ---- stage this slice of x: 8 threads per batch row, 16 B each per pass ----
-  {
+  const int lq = lane & 31, hh = lane >> 5;
+  const int span = Ks / 4;          // columns of this wave
+  const int steps = span / 16;      // k-steps of this wave
+
+  // Weight rows of a block and their loads.  The first two batches of a block
+  // are requested before the previous block's hand-off (and, for the first
+  // block, before x is staged), so their HBM latency is covered.
+  const bf16_t* wg = nullptr;
+  const bf16_t* wu = nullptr;
+  bf16x8 wv[2][kU], uv[2][SWIGLU ? kU : 1];
+  auto set_rows = [&](int nb) {
+    const int n = nb * kNB + lq;
+    wg = W + static_cast<size_t>(n < N ? n : N - 1) * K + k0 + w * span + 8 * hh;
+    if (SWIGLU) wu = wg + static_cast<size_t>(N) * K;
+  };
+  auto fetch = [&](int buf, int s0) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (s0 + u < steps) {  // wave-uniform
+        wv[buf][u] = *reinterpret_cast<const bf16x8*>(wg + 16 * (s0 + u));
+        if (SWIGLU) uv[buf][u] = *reinterpret_cast<const bf16x8*>(wu + 16 * (s0 + u));
+      }
+  };
+  if (nb0 < NB) {
+    set_rows(nb0);
+    fetch(0, 0);
+    fetch(1, kU);
+  }
+
+  // ---- stage this slice of x ----
+  // Without the fused norm the slice is a plain copy: LDS-DMA (global_load_lds, 16 B per
+  // lane, no VGPR round trip), one wave instruction per KB of a row, every one of them in
+  // flight at once.  Rows >= M re-read row 0: a column of the B operand only reaches its
+  // own output column, which is never written.
+  if (!NORM && Ks % 512 == 0) {
+    const int per_row = Ks / 512;  // wave instructions per row
+    for (int m = w; m < kMB; m += 4) {
+      const bf16_t* xr = x + static_cast<size_t>(m < M ? m : 0) * K + k0 + 8 * lane;
+      bf16_t* dst = xs + static_cast<size_t>(m) * pitch;
+      for (int j = 0; j < per_row; ++j)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xr + 512 * j),
+                                         (__attribute__((address_space(3))) void*)(dst + 512 * j), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    // 8 threads per batch row, 8 x 16 B in flight each
+    constexpr int SU = 8;
     const int m = tid >> 3, sub = tid & 7;
     const int chunks = Ks / 8;
     const bool row = m < M;
     const bf16_t* xr = x + static_cast<size_t>(row ? m : 0) * K + k0;
     const bf16_t* rr = res ? res + static_cast<size_t>(row ? m : 0) * K + k0 : nullptr;
+    const bool hw = NORM && rr && h_out && nb0 == 0;  // the new residual stream, once per slice
     float ss = 0.f;
-    for (int c = sub; c < chunks; c += 8) {
-      bf16x8 v = bf16x8{};
-      if (row) {
-        v = *reinterpret_cast<const bf16x8*>(xr + 8 * c);
-        if (NORM) {
-          if (rr) {
-            const bf16x8 r = *reinterpret_cast<const bf16x8*>(rr + 8 * c);
+    for (int c0 = sub; c0 < chunks; c0 += 8 * SU) {
+      bf16x8 xv[SU], rv[NORM ? SU : 1], gv[NORM ? SU : 1];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) + bf2f(r[j]));
-            if (h_out && nb0 == 0)  // the new residual stream, once per slice
-              *reinterpret_cast<bf16x8*>(h_out + static_cast<size_t>(m) * K + k0 + 8 * c) = v;
+      for (int u = 0; u < SU; ++u) {
+        const int c = c0 + 8 * u;
+        xv[u] = bf16x8{};
+        if (row && c < chunks) {
+          xv[u] = *reinterpret_cast<const bf16x8*>(xr + 8 * c);
+          if (NORM) {
+            rv[NORM ? u : 0] = rr ? *reinterpret_cast<const bf16x8*>(rr + 8 * c) : bf16x8{};
+            gv[NORM ? u : 0] = *reinterpret_cast<const bf16x8*>(g + k0 + 8 * c);
           }
-          const bf16x8 gw = *reinterpret_cast<const bf16x8*>(g + k0 + 8 * c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int c = c0 + 8 * u;
+        if (c >= chunks) break;
+        bf16x8 v = xv[u];
+        if (NORM && row) {
+          if (rr) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) + bf2f(rv[NORM ? u : 0][j]));
+            if (hw) *reinterpret_cast<bf16x8*>(h_out + static_cast<size_t>(m) * K + k0 + 8 * c) = v;
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float f = bf2f(v[j]);
             ss += f * f;
-            v[j] = f2bf(f * bf2f(gw[j]));
+            v[j] = f2bf(f * bf2f(gv[NORM ? u : 0][j]));
           }
         }
+        *reinterpret_cast<bf16x8*>(xs + static_cast<size_t>(m) * pitch + 8 * c) = v;
       }
-      *reinterpret_cast<bf16x8*>(xs + static_cast<size_t>(m) * pitch + 8 * c) = v;
     }
     if (NORM) {
       ss += __shfl_xor(ss, 1, kWave);
@@ -141,29 +199,12 @@ __global__ __launch_bounds__(kT) void skinny_kernel(
   }
   __syncthreads();
 
-  const int lq = lane & 31, hh = lane >> 5;
-  const int span = Ks / 4;          // columns of this wave
-  const int steps = span / 16;      // k-steps of this wave
   const bf16_t* xw = xs + static_cast<size_t>(lq) * pitch + w * span + 8 * hh;
 
   for (int nb = nb0; nb < NB; nb += nb_step) {
-    const int n = nb * kNB + lq;
-    const bool nvalid = n < N;
-    const bf16_t* wg = W + static_cast<size_t>(nvalid ? n : N - 1) * K + k0 + w * span + 8 * hh;
-    const bf16_t* wu = SWIGLU ? wg + static_cast<size_t>(N) * K : nullptr;
-
     f32x16 acc[TILES];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) acc[t] = f32x16{};
-    bf16x8 wv[2][kU], uv[2][SWIGLU ? kU : 1];
-    auto fetch = [&](int buf, int s0) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (s0 + u < steps) {  // wave-uniform
-          wv[buf][u] = *reinterpret_cast<const bf16x8*>(wg + 16 * (s0 + u));
-          if (SWIGLU) uv[buf][u] = *reinterpret_cast<const bf16x8*>(wu + 16 * (s0 + u));
-        }
-    };
     auto consume = [&](int buf, int s0) {
 #pragma unroll
       for (int u = 0; u < kU; ++u)
@@ -173,12 +214,16 @@ __global__ __launch_bounds__(kT) void skinny_kernel(
           if (SWIGLU) acc[TILES - 1] = mfma(uv[buf][SWIGLU ? u : 0], xf, acc[TILES - 1]);
         }
     };
-    fetch(0, 0);
-    for (int s0 = 0; s0 < steps; s0 += 2 * kU) {
-      fetch(1, s0 + kU);
+    for (int s0 = 0; s0 < steps; s0 += 2 * kU) {  // batches [s0, s0 + kU) and [s0 + kU, s0 + 2 kU) are in flight
       consume(0, s0);
       fetch(0, s0 + 2 * kU);
       consume(1, s0 + kU);
+      fetch(1, s0 + 3 * kU);
+    }
+    if (nb + nb_step < NB) {  // the next block's first batches
+      set_rows(nb + nb_step);
+      fetch(0, 0);
+      fetch(1, kU);
     }
 
     // ---- the four waves' tiles meet in wave 0: (2, 3) -> (0, 1), then 1 -> 0 ----
@@ -274,8 +319,11 @@ __global__ __launch_bounds__(kT) void skinny_kernel(
   }
 }
 
-// K slices for [N, K] at batch M: slices of <= kMaxSlice columns (multiples of
-// 64), and more of them while the grid would not fill the chip.
+// K slices for [N, K]: the fewest slices of <= kMaxSlice columns (multiples of
+// 64).  A split costs every row block a publish -> ticket -> re-read chain of
+// dependent memory round trips (~4 us), more than a workgroup that streams a
+// few hundred KB on its own saves by sharing them; only a projection with too
+// few row blocks to occupy a quarter of the CUs is split further.
 int pick_slices(int N, int K, int cus) {
   const int nb = (N + kNB - 1) / kNB;
   int best = 0;
@@ -286,7 +334,7 @@ int pick_slices(int N, int K, int cus) {
     if (best == 0) best = s;
     if (ks < 256) break;
     best = s;
-    if (nb * s >= cus) break;
+    if (nb * s >= cus / 4) break;
   }
   return best;
 }
@@ -334,7 +382,7 @@ KGWE_API int64_t kgwe_decode_skinny_workspace(int N, int K, int swiglu, int cus)
 }
 
 // x [M, K] bf16 (8 < M <= 32 also takes M <= 8), W [N, K] (SWIGLU: [2N, K]),
-// y [M, N] (may be null in ARGMAX mode), K % 64 == 0.  NORM modes: res [M, K]
+// y [M, N] (may be null in the ARGMAX modes 4 and 5), K % 64 == 0.  NORM modes: res [M, K]
 // or null, g [K], h_out [M, K] or null (must not alias x / res).  ARGMAX:
 // best [M * kgwe_decode_skinny_blocks(N)] u64, one partial maximum per row
 // block, reduced by kgwe_decode_argmax_finish.  `workspace` as sized by
@@ -346,7 +394,7 @@ KGWE_API int kgwe_decode_skinny(const void* x, const void* res, const void* g, v
                                 int K, int mode, int cus, hipStream_t s) {
   if (M <= 0 || M > kMB || N <= 0 || K <= 0 || K % 64 || !workspace) return -1;
   if ((mode & kNorm) && !g) return -1;
-  if (mode == kNormArgmax && !best) return -1;
+  if ((mode & kArgmax) && !best) return -1;
   if (cus <= 0) cus = 256;
   const int KS = pick_slices(N, K, cus);
   if (KS <= 0) return -1;
@@ -364,6 +412,7 @@ KGWE_API int kgwe_decode_skinny(const void* x, const void* res, const void* g, v
     case kPlain: return launch<kPlain>(x, res, g, h_out, eps, W, y, best, part, tickets, M, N, K, KS, NB, grid, s);
     case kNorm: return launch<kNorm>(x, res, g, h_out, eps, W, y, best, part, tickets, M, N, K, KS, NB, grid, s);
     case kSwiglu: return launch<kSwiglu>(x, res, g, h_out, eps, W, y, best, part, tickets, M, N, K, KS, NB, grid, s);
+    case kArgmax: return launch<kArgmax>(x, res, g, h_out, eps, W, y, best, part, tickets, M, N, K, KS, NB, grid, s);
     case kNormSwiglu:
       return launch<kNormSwiglu>(x, res, g, h_out, eps, W, y, best, part, tickets, M, N, K, KS, NB, grid, s);
     case kNormArgmax:
