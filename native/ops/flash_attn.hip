@@ -110,7 +110,7 @@ __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (
 
 // Raise a wave's issue priority over its MFMA chains and drop it for the
 // softmax, so each SIMD's arbiter keeps the matrix pipe fed from whichever of
-// its two waves is in an MFMA phase.  Measured (tools/gpu_fa_variants.sh, B=2
+// its two waves is in an MFMA phase.  Measured (tools/gpu.sh fa-variants, B=2
 // S=4096 causal): backward 1.142 -> 1.128 ms, forward 0.369 -> 0.384 ms — so
 // on in the dQ and dK/dV kernels, off in the forward.
 #ifndef FA_MFMA_PRIO_FWD

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build one timing binary per flash-attention compile-time variant into
-# fa_var_bin/ (git-ignored, travels with gpurun); run with tools/gpu_fa_variants.sh.
+# fa_var_bin/ (git-ignored, travels with gpurun); run with `tools/gpu.sh fa-variants`.
 # "base" is the shipped configuration; every other binary is compared to it.
 set -e
 cd "$(dirname "$0")/.."

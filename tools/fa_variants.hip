@@ -1,6 +1,6 @@
 // Standalone timing harness for compile-time variants of native/ops/flash_attn.hip
 // (no Python on the timed path).  Build one binary per variant with -D flags,
-// e.g. tools/gpu_fa_variants.sh; each run times fwd and fwd+bwd at the
+// and run them with `tools/gpu.sh fa-variants`; each run times fwd and fwd+bwd at the
 // Llama-3-8B attention shape (B=2, S=4096, 32 q / 8 kv heads, d=128, causal)
 // and dumps O / dQ / dK / dV checksums plus raw outputs so a variant can be
 // compared bit-for-bit (or to bf16 rounding) against the baseline binary.

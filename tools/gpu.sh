@@ -17,6 +17,7 @@
 #                         rocprofv3 kernel trace + stats of a python program
 #   wgrad [bench args]    weight-gradient GEMM: numerics, then tools/wgrad_kernel_bench.py
 #   attn                  attention numerics, then tools/attn_bench.py
+#   fa-variants           time / compare the flash-attention compile-time variants in fa_var_bin/
 #   attn-modes M...       forward attention: numerics tests + timing at B = 2 / 4, once per KGWE_FA_FWD value
 #                         (selects a kernel only with profiles/r03_attn/skew_kernel.patch applied; plain: attn-modes 0)
 #   ops                   tools/ops_bench.py (every hand-written op against its roofline)
@@ -105,6 +106,18 @@ attn)
   tail -3 gpurun_out/attn_test.log
   run 200 gpurun_out/attn_bench.log python tools/attn_bench.py
   grep -v amdgpu.ids gpurun_out/attn_bench.log | tail -8 ;;
+fa-variants)
+  # compile-time variants of native/ops/flash_attn.hip built by tools/build_fa_variants.sh into
+  # fa_var_bin/: "base" first (it dumps its outputs), every other binary is compared with it;
+  # FA_B / FA_CAUSAL in the environment choose batch and masking
+  [ -x fa_var_bin/fa_base ] || { echo "run tools/build_fa_variants.sh first"; exit 1; }
+  run 120 gpurun_out/fa_var_base.log fa_var_bin/fa_base base
+  tail -1 gpurun_out/fa_var_base.log
+  for b in fa_var_bin/fa_*; do
+    tag=${b#fa_var_bin/fa_}; [ "$tag" = base ] && continue
+    run 120 "gpurun_out/fa_var_$tag.log" "$b" "$tag" /tmp/fa_base.bin
+    tail -1 "gpurun_out/fa_var_$tag.log"
+  done ;;
 attn-modes)
   # forward kernel variants (KGWE_FA_FWD, read once per process): numerics, then timing
   for mode in "$@"; do
