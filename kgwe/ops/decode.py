@@ -229,10 +229,13 @@ _SKINNY_WS: dict = {}
 
 def _skinny_workspace(x: torch.Tensor, N: int, K: int, swiglu: bool) -> torch.Tensor:
     """Split-K partials + tickets of the MFMA kernel for this shape, zeroed
-    once (every launch leaves the tickets at zero), one per stream: launches
-    that share it are ordered by the stream."""
+    once (every launch leaves the tickets at zero).  One per device and shape:
+    launches that share it must be ordered by their stream, as the layers of
+    one decode step are.  (Not per stream: a hipGraph capture runs on a stream
+    of its own, and a workspace first created there would be allocated — and
+    zero-filled again on every replay — inside the graph.)"""
     cus = max_wgs() // 8
-    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream, N, K, swiglu, cus)
+    key = (x.device, N, K, swiglu, cus)
     ws = _SKINNY_WS.get(key)
     if ws is None:
         nbytes = lib().kgwe_decode_skinny_workspace(N, K, int(swiglu), cus)
