@@ -142,10 +142,17 @@ __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
   float acc[kPer];
 #pragma unroll
   for (int t = 0; t < kPer; ++t) acc[t] = 0.0f;
-  for (int t0 = start; t0 < end; t0 += 64) {
-    __syncthreads();  // qs written / previous tile consumed
-    constexpr int kChunks = 64 * D / 8;
-    for (int idx = threadIdx.x; idx < kChunks; idx += 64 * G) {
+  // K / V tiles of 64 keys go HBM -> registers -> LDS, and the loads of tile t + 1 are issued
+  // before the math of tile t: with the loads inside the tile loop every tile exposed a full
+  // memory round trip (a split of 256 keys is four of them).
+  constexpr int kChunks = 64 * D / 8;
+  constexpr int NCH = kChunks / (64 * G);  // 16-B chunks per thread per matrix and tile
+  static_assert(kChunks % (64 * G) == 0, "tile chunks divide evenly over the workgroup");
+  bf16x8 kr[NCH], vr[NCH];
+  auto load_tile = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = threadIdx.x + i * 64 * G;
       const int r = idx / (D / 8), c = (idx % (D / 8)) * 8;
       const int key = t0 + r;
       bf16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -170,10 +177,22 @@ __global__ __launch_bounds__(64 * G) void decode_attn_kernel(
         kv = *reinterpret_cast<const bf16x8*>(kbase + static_cast<int64_t>(key) * D + c);
         vv = *reinterpret_cast<const bf16x8*>(vbase + static_cast<int64_t>(key) * D + c);
       }
-      *reinterpret_cast<bf16x8*>(&ks[r][c]) = kv;
-      *reinterpret_cast<bf16x8*>(&vs[r][c]) = vv;
+      kr[i] = kv;
+      vr[i] = vv;
+    }
+  };
+  if (start < end) load_tile(start);
+  for (int t0 = start; t0 < end; t0 += 64) {
+    __syncthreads();  // qs written / previous tile consumed
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = threadIdx.x + i * 64 * G;
+      const int r = idx / (D / 8), c = (idx % (D / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&ks[r][c]) = kr[i];
+      *reinterpret_cast<bf16x8*>(&vs[r][c]) = vr[i];
     }
     __syncthreads();
+    if (t0 + 64 < end) load_tile(t0 + 64);  // lands during this tile's math
     const int key = t0 + lane;
     float s = -INFINITY;
     if (key < end) {

@@ -17,6 +17,7 @@
 #                         rocprofv3 kernel trace + stats of a python program
 #   wgrad [bench args]    weight-gradient GEMM: numerics, then tools/wgrad_kernel_bench.py
 #   attn                  attention numerics, then tools/attn_bench.py
+#   decode-bench [M]      decode projections (batch M, default 32) and decode attention, kernel by kernel
 #   fa-variants           time / compare the flash-attention compile-time variants in fa_var_bin/
 #   attn-modes M...       forward attention: numerics tests + timing at B = 2 / 4, once per KGWE_FA_FWD value
 #                         (selects a kernel only with profiles/r03_attn/skew_kernel.patch applied; plain: attn-modes 0)
@@ -106,6 +107,10 @@ attn)
   tail -3 gpurun_out/attn_test.log
   run 200 gpurun_out/attn_bench.log python tools/attn_bench.py
   grep -v amdgpu.ids gpurun_out/attn_bench.log | tail -8 ;;
+decode-bench)
+  # serving-batch decode kernels one by one: projections against the library GEMM, attention split sweep
+  run 300 gpurun_out/decode_bench.log python tools/skinny_bench.py "$@"
+  grep "^M=" gpurun_out/decode_bench.log ;;
 fa-variants)
   # compile-time variants of native/ops/flash_attn.hip built by tools/build_fa_variants.sh into
   # fa_var_bin/: "base" first (it dumps its outputs), every other binary is compared with it;
