@@ -326,9 +326,11 @@ KGWE_API int64_t kgwe_decode_attn_workspace(int B, int Hq, int D, int splits) {
 // Split count for a cache of Smax keys: enough workgroups to cover the 256
 // CUs about twice, at least 64 keys per split.
 KGWE_API int kgwe_decode_attn_splits(int B, int Hkv, int Smax) {
-  // ~1024 workgroups: at a serving batch (B = 32, 8 kv heads) 4 splits measured 23.0 us per
-  // layer against 31.8 with 2 and 25.8 with 8 (640 of 1,024 positions cached)
-  const int want = (1024 + B * Hkv - 1) / (B * Hkv);
+  // ~1024 workgroups up to a serving batch of 32 rows x 8 kv heads (4 splits: 22.0 us per layer
+  // against 25.2 with 2 and 25.9 with 8; 640 of 1,024 positions cached); past that one split per
+  // (row, kv head) is best: no partials to publish and merge (64 rows: 28.2 us with 1 split, 37.0
+  // with 2; 128 rows: 44.8 against 63.4)
+  const int want = B * Hkv >= 512 ? 1 : (1024 + B * Hkv - 1) / (B * Hkv);
   const int most = (Smax + 63) / 64;
   return std::max(1, std::min({want, most, 64}));  // the merge holds one split per lane
 }
