@@ -175,8 +175,11 @@ class Generator:
             else:
                 xn, residual = K.rmsnorm(h, layer.attention_norm, c.norm_eps, residual=residual)
             qkv = K.linear(xn, layer.attention.wqkv)
-            q = dec.rope_append(qkv, self.pos, self.cos, self.sin, self.kv[0, i], self.kv[1, i], hq, hkv, d)
-            o = self.attn(q, self.kv[0, i], self.kv[1, i], self.lens)
+            if self.dev.type == "cuda":  # RoPE + cache append inside the attention launch
+                o = self.attn.rope_attend(qkv, self.cos, self.sin, self.kv[0, i], self.kv[1, i], self.lens)
+            else:
+                q = dec.rope_append(qkv, self.pos, self.cos, self.sin, self.kv[0, i], self.kv[1, i], hq, hkv, d)
+                o = self.attn(q, self.kv[0, i], self.kv[1, i], self.lens)
             a = K.linear(o.view(self.B, -1), layer.attention.wo)
             xn, residual = K.rmsnorm(a, layer.ffn_norm, c.norm_eps, residual=residual)
             h = layer.feed_forward(xn)
