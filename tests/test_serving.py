@@ -65,6 +65,36 @@ def test_each_client_gets_its_private_generators_tokens(model):
         t.join(5)
 
 
+def test_a_burst_of_same_shape_requests_shares_one_prefill_pass(model):
+    """Requests that wait together and have one prompt length are admitted in
+    ONE prefill pass over consecutive slots; a request of another length gets
+    its own.  Everybody still receives its private generator's tokens."""
+    V = model.cfg.vocab_size
+    g = torch.Generator().manual_seed(1)
+    srv = BatchServer(model, 4, 2, 96, flush=4, graph=False)
+    addr = srv.listen("127.0.0.1:0")   # accepting, not serving yet: the requests queue up
+    reqs = [(torch.randint(0, V, (2, P), generator=g).tolist(), n) for P, n in ((16, 7), (16, 11), (16, 3), (24, 5))]
+    out = [None] * len(reqs)
+    ths = [threading.Thread(target=lambda i=i: out.__setitem__(i, client.generate(reqs[i][0], reqs[i][1], addr)))
+           for i in range(len(reqs))]
+    [x.start() for x in ths]
+    deadline = time.time() + 10
+    while srv.pending.qsize() < len(reqs) and time.time() < deadline:
+        time.sleep(0.01)
+    assert srv.pending.qsize() == len(reqs)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    try:
+        [x.join(60) for x in ths]
+        for (prompt, n), res in zip(reqs, out):
+            assert res is not None and res["tokens"] == _private(model, prompt, n)
+        st = client.call(addr, {"op": "stats"})
+        assert st["served"] == 4 and st["prefill_passes"] == 2   # three of length 16 together, one of 24
+    finally:
+        srv.stop()
+        t.join(5)
+
+
 def test_bad_requests_are_refused_without_disturbing_the_batch(model):
     srv, addr, t = _serve(model, slots=2, rows=1)
     try:
