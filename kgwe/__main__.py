@@ -15,6 +15,7 @@ COMMANDS = {
     "bench-cluster": "kgwe.bench.cluster",  # stock kube vs kgwe on one trace (simulated)
     "bench-scaling": "kgwe.bench.scaling",  # bench.py at 1/2/4/8 GPUs -> scaling curve
     "bench-infer": "kgwe.bench.infer",  # bf16 decode server / co-located servers on one GPU
+    "serve-batch": "kgwe.serving.batch_server",  # one continuous-batching server per share group
     "busbw": "kgwe.parallel.busbw",            # RCCL all-reduce bus bandwidth sweep
     "crds": "kgwe.api.crds",                   # render CRD YAML
     "launch": "kgwe.launch",                   # container entrypoint (placement env)
